@@ -1,0 +1,161 @@
+"""ctypes binding of the C ABI in ``include/hashnerf_amd.h``.
+
+This is the drop-in boundary the reference's Python would bind: plain
+``extern "C"`` entry points taking device pointers, sizes and a hipStream_t.
+There is deliberately NO CPU fallback: if the HIP library is missing or the
+tensors are not on a ROCm device, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libhashnerf_amd.so")
+MAX_LEVELS = 32
+MLP_PARAMS = 9344
+MLP_PACKED_FLOATS = 24064
+
+_lib = None
+
+
+class HnGrid(C.Structure):
+    _fields_ = [("n_levels", C.c_int32), ("n_features", C.c_int32),
+                ("log2_hashmap_size", C.c_int32), ("reserved", C.c_int32),
+                ("box_min", C.c_float * 3), ("box_max", C.c_float * 3),
+                ("grid_size", (C.c_float * 3) * MAX_LEVELS)]
+
+
+class HnMlp(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("sigma0", "sigma1", "color0", "color1", "color2")]
+
+
+class HnMlpGrad(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("sigma0", "sigma1", "color0", "color1", "color2")]
+
+
+class HnRenderCfg(C.Structure):
+    _fields_ = [("grid", HnGrid), ("n_samples", C.c_int32), ("n_importance", C.c_int32),
+                ("white_bkgd", C.c_int32), ("lindisp", C.c_int32), ("perturb", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
+
+
+_P = C.c_void_p
+
+
+class HnRenderFwdArgs(C.Structure):
+    _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("t_vals", _P), ("t_rand", _P), ("u", _P),
+                ("noise_c", _P), ("noise_f", _P), ("table", _P), ("coarse", HnMlp), ("fine", HnMlp),
+                ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
+                ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
+                ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P)]
+
+
+class HnRenderBwdArgs(C.Structure):
+    _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("noise_c", _P), ("noise_f", _P), ("table", _P),
+                ("coarse", HnMlp), ("fine", HnMlp), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P),
+                ("raw_f", _P), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
+                ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
+                ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
+
+
+# name -> (restype, argtypes); must match include/hashnerf_amd.h exactly.
+SIGNATURES = {
+    "hn_abi_version": (C.c_int32, []),
+    "hn_status_string": (C.c_char_p, [C.c_int32]),
+    "hn_encode_fwd": (C.c_int32, [C.POINTER(HnGrid), _P, C.c_int64, _P, _P, _P, _P]),
+    "hn_encode_bwd": (C.c_int32, [C.POINTER(HnGrid), _P, C.c_int64, _P, _P, _P]),
+    "hn_sh_fwd": (C.c_int32, [_P, C.c_int64, _P, _P]),
+    "hn_mlp_workspace_bytes": (C.c_size_t, []),
+    "hn_mlp_fwd": (C.c_int32, [C.POINTER(HnMlp), _P, C.c_int64, _P, _P, C.c_size_t, _P]),
+    "hn_mlp_bwd": (C.c_int32, [C.POINTER(HnMlp), _P, _P, C.c_int64, _P, C.POINTER(HnMlpGrad), _P,
+                               C.c_size_t, _P]),
+    "hn_composite_fwd": (C.c_int32, [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P,
+                                     _P, _P, _P, _P]),
+    "hn_composite_bwd": (C.c_int32, [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P,
+                                     _P, _P, _P, _P]),
+    "hn_sample_pdf": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P]),
+    "hn_render_workspace_bytes": (C.c_size_t, [C.POINTER(HnRenderCfg), C.c_int64]),
+    "hn_render_fwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderFwdArgs), _P,
+                                  C.c_size_t, _P]),
+    "hn_render_bwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderBwdArgs), _P,
+                                  C.c_size_t, _P]),
+}
+
+
+def lib():
+    """Load (once) the HIP library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"hashnerf_amd: HIP library not built ({LIB_PATH}); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` -- there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = lib().hn_status_string(status).decode()
+        raise RuntimeError(f"hashnerf_amd.{what} failed: {msg} (status {status})")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream(device: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*tensors: torch.Tensor):
+    """The product path runs only on a ROCm device: fail loudly otherwise."""
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("hashnerf_amd: tensors must live on a ROCm (HIP) device; "
+                               "the reference CPU path is not part of this package")
+        if t.dtype != torch.float32:
+            raise TypeError(f"hashnerf_amd: expected float32, got {t.dtype}")
+
+
+def contig(t: Optional[torch.Tensor]):
+    return None if t is None else t.contiguous()
+
+
+def make_grid(n_levels, n_features, log2T, box_min, box_max, grid_sizes) -> HnGrid:
+    g = HnGrid()
+    g.n_levels, g.n_features, g.log2_hashmap_size = int(n_levels), int(n_features), int(log2T)
+    bmin = [float(v) for v in box_min]
+    bmax = [float(v) for v in box_max]
+    for a in range(3):
+        g.box_min[a] = bmin[a]
+        g.box_max[a] = bmax[a]
+    for l, row in enumerate(grid_sizes):
+        for a in range(3):
+            g.grid_size[l][a] = float(row[a])
+    return g
+
+
+def make_mlp(ws) -> HnMlp:
+    m = HnMlp()
+    for k, t in zip(("sigma0", "sigma1", "color0", "color1", "color2"), ws):
+        setattr(m, k, t.data_ptr())
+    return m
+
+
+def make_mlp_grad(gs) -> HnMlpGrad:
+    m = HnMlpGrad()
+    for k, t in zip(("sigma0", "sigma1", "color0", "color1", "color2"), gs):
+        setattr(m, k, t.data_ptr())
+    return m

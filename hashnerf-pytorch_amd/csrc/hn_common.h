@@ -1,0 +1,242 @@
+// hn_common.h -- device building blocks shared by every HashNeRF kernel (gfx950).
+//
+// Compiled with -ffp-contract=off: every fp32 expression below rounds after
+// each operation exactly like the reference's sequence of eager torch ops, so
+// the hash-grid encoding and SH features are bit-identical to the reference.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hashnerf_amd.h"
+
+#define HN_DEV __device__ __forceinline__
+
+namespace hn {
+
+constexpr uint32_t kPrimeY = 2654435761u;   // hash_encoding.py:7
+constexpr uint32_t kPrimeZ = 805459861u;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Kernel-argument copy of hn_grid (passed by value).
+struct GridArgs {
+  int32_t n_levels;
+  int32_t log2T;
+  float bmin[3];
+  float bmax[3];
+  float gs[HN_MAX_LEVELS][3];
+};
+
+inline GridArgs make_grid_args(const hn_grid& g) {
+  GridArgs a;
+  a.n_levels = g.n_levels;
+  a.log2T = g.log2_hashmap_size;
+  for (int i = 0; i < 3; ++i) { a.bmin[i] = g.box_min[i]; a.bmax[i] = g.box_max[i]; }
+  for (int l = 0; l < HN_MAX_LEVELS; ++l)
+    for (int i = 0; i < 3; ++i) a.gs[l][i] = g.grid_size[l][i];
+  return a;
+}
+
+// torch.clamp(x, min=lo, max=hi) with NaN propagation (hash_encoding.py:69).
+HN_DEV float clamp_t(float x, float lo, float hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+
+// One hash level of one point (hash_encoding.py:59-82 + :112-128 + :143).
+//   xc: clamped point (corners), x: unclamped point (trilinear weights).
+// Outputs the 8 hashed row indices (corner c = 4i+2j+k) and the weights.
+struct Voxel {
+  uint32_t h[8];
+  float w[3];
+};
+
+HN_DEV void voxel_level(const float x[3], const float xc[3], const float gs[3],
+                        const float bmin[3], uint32_t mask, Voxel& v) {
+  uint32_t c[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float q = (xc[a] - bmin[a]) / gs[a];
+    const int32_t i = (int32_t)floorf(q);                 // floor(...).int()
+    const float vmin = (float)i * gs[a] + bmin[a];        // idx * grid + min
+    const float vmax = vmin + gs[a];                      // + 1.0 * grid
+    v.w[a] = (x[a] - vmin) / (vmax - vmin);
+    c[a] = (uint32_t)i;
+  }
+  const uint32_t x0 = c[0], x1 = c[0] + 1u;               // prime 1
+  const uint32_t y0 = c[1] * kPrimeY, y1 = (c[1] + 1u) * kPrimeY;
+  const uint32_t z0 = c[2] * kPrimeZ, z1 = (c[2] + 1u) * kPrimeZ;
+  v.h[0] = (x0 ^ y0 ^ z0) & mask;
+  v.h[1] = (x0 ^ y0 ^ z1) & mask;
+  v.h[2] = (x0 ^ y1 ^ z0) & mask;
+  v.h[3] = (x0 ^ y1 ^ z1) & mask;
+  v.h[4] = (x1 ^ y0 ^ z0) & mask;
+  v.h[5] = (x1 ^ y0 ^ z1) & mask;
+  v.h[6] = (x1 ^ y1 ^ z0) & mask;
+  v.h[7] = (x1 ^ y1 ^ z1) & mask;
+}
+
+// trilinear_interp (hash_encoding.py:130-163): x first, then y, then z.
+HN_DEV float trilerp(const float e[8], const float w[3]) {
+  const float ax = 1.f - w[0], ay = 1.f - w[1], az = 1.f - w[2];
+  const float c00 = e[0] * ax + e[4] * w[0];
+  const float c01 = e[1] * ax + e[5] * w[0];
+  const float c10 = e[2] * ax + e[6] * w[0];
+  const float c11 = e[3] * ax + e[7] * w[0];
+  const float c0 = c00 * ay + c10 * w[1];
+  const float c1 = c01 * ay + c11 * w[1];
+  return c0 * az + c1 * w[2];
+}
+
+// d feat / d e_c = ((g * az) * ay) * ax: autograd's multiplication order.
+HN_DEV void trilerp_bwd(float g, const float w[3], float out[8]) {
+  const float ax = 1.f - w[0], ay = 1.f - w[1], az = 1.f - w[2];
+  const float gz0 = g * az, gz1 = g * w[2];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float gzy = ((c & 1) ? gz1 : gz0) * ((c & 2) ? w[1] : ay);
+    out[c] = gzy * ((c & 4) ? w[0] : ax);
+  }
+}
+
+HN_DEV void atomic_add_f32(float* p, float v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Gather one level's two features for a point: table_l is [2^T][2].
+HN_DEV void encode_level(const float* __restrict__ table_l, const Voxel& v, float& f0, float& f1) {
+  float e0[8], e1[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float2 t = *reinterpret_cast<const float2*>(table_l + 2 * (size_t)v.h[c]);
+    e0[c] = t.x;
+    e1[c] = t.y;
+  }
+  f0 = trilerp(e0, v.w);
+  f1 = trilerp(e1, v.w);
+}
+
+// Same, addressed as uniform table base + 32-bit byte offset (row r of level
+// l sits at byte (((l << T) + r) * 8)); lets hipcc use the SGPR-base +
+// 32-bit-VGPR-offset addressing mode instead of 64-bit per-lane addresses.
+HN_DEV float2 ld_row(const float* __restrict__ table, uint32_t byte_off) {
+  return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(table) + byte_off);
+}
+HN_DEV void encode_level_off(const float* __restrict__ table, uint32_t lvl_row0, const Voxel& v,
+                             float& f0, float& f1) {
+  float e0[8], e1[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float2 t = ld_row(table, (lvl_row0 + v.h[c]) * 8u);
+    e0[c] = t.x;
+    e1[c] = t.y;
+  }
+  f0 = trilerp(e0, v.w);
+  f1 = trilerp(e1, v.w);
+}
+HN_DEV void atomic_add_row(float* table, uint32_t byte_off, float g0, float g1) {
+  float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(table) + byte_off);
+  atomic_add_f32(p, g0);
+  atomic_add_f32(p + 1, g1);
+}
+
+// SHEncoder.forward degree 4 (spherical_harmonic.py:65-103); constants are
+// rounded to fp32 first, exactly as torch does for python-scalar * tensor.
+HN_DEV void sh16(float x, float y, float z, float o[16]) {
+  const float C0 = 0.28209479177387814f, C1 = 0.4886025119029199f;
+  const float C2_0 = 1.0925484305920792f, C2_1 = -1.0925484305920792f,
+              C2_2 = 0.31539156525252005f, C2_3 = -1.0925484305920792f,
+              C2_4 = 0.5462742152960396f;
+  const float C3_0 = -0.5900435899266435f, C3_1 = 2.890611442640554f,
+              C3_2 = -0.4570457994644658f, C3_3 = 0.3731763325901154f,
+              C3_4 = -0.4570457994644658f, C3_5 = 1.445305721320277f,
+              C3_6 = -0.5900435899266435f;
+  const float xx = x * x, yy = y * y, zz = z * z;
+  const float xy = x * y, yz = y * z, xz = x * z;
+  o[0] = C0;
+  o[1] = -C1 * y;
+  o[2] = C1 * z;
+  o[3] = -C1 * x;
+  o[4] = C2_0 * xy;
+  o[5] = C2_1 * yz;
+  o[6] = C2_2 * (2.0f * zz - xx - yy);
+  o[7] = C2_3 * xz;
+  o[8] = C2_4 * (xx - yy);
+  o[9] = C3_0 * y * (3.f * xx - yy);
+  o[10] = C3_1 * xy * z;
+  o[11] = C3_2 * y * (4.f * zz - xx - yy);
+  o[12] = C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+  o[13] = C3_4 * x * (4.f * zz - xx - yy);
+  o[14] = C3_5 * z * (xx - yy);
+  o[15] = C3_6 * x * (xx - 3.f * yy);
+}
+
+// ---------------------------------------------------------------------------
+// Wave (64-lane) primitives
+// ---------------------------------------------------------------------------
+HN_DEV int lane_id() { return (int)__lane_id(); }
+
+template <typename T>
+HN_DEV T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Inclusive scans across the 64 lanes (Hillis-Steele).
+HN_DEV double wave_incl_sum(double v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(v, o, 64);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+HN_DEV double wave_incl_prod(double v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(v, o, 64);
+    if (l >= o) v *= t;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA 32x32x2 f32 (exact f32 FMA chain).  Lane l: i = l & 31, h = l >> 5.
+//   A operand: A[i][k=h]   B operand: B[k=h][j=i]
+//   C/D: col = l & 31, row(r) = (r & 3) + 8 * (r >> 2) + 4 * h
+// ---------------------------------------------------------------------------
+HN_DEV f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+HN_DEV constexpr int row_of(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// Level handled by register pair (2m, 2m+1) of lane half h in the 32-feature
+// tile layout: feature ROW(2m,h) = 2 * lev(m,h).
+HN_DEV constexpr int tile_level(int m, int h) { return (m & 1) + 4 * (m >> 1) + 2 * h; }
+
+// Order this wave's LDS writes before its later LDS reads of other lanes' data
+// (LDS executes one wave's instructions in order; this pins the compiler).
+HN_DEV void lds_fence_wave() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// Hide a uniform pointer's value from the optimiser.  Used at the top of tile
+// loops so hipcc cannot hoist hundreds of loop-invariant weight-fragment loads
+// out of the loop (which blows the register file and spills).
+template <typename T>
+HN_DEV T* opaque_ptr(T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+inline int32_t hip_status(hipError_t e) { return e == hipSuccess ? HN_OK : HN_E_HIP + (int32_t)e; }
+
+HN_DEV f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+}  // namespace hn

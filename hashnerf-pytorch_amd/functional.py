@@ -1,0 +1,241 @@
+"""torch.autograd wrappers around the HIP C ABI (one Function per entry point).
+
+PyTorch supplies device memory, the current HIP stream and autograd
+plumbing; every byte of arithmetic on the hot path runs in the gfx950 HIP
+library.  Gradient buffers are zero-initialised here and accumulated (+=) by
+the kernels, mirroring the C ABI contract.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib as L
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def _no_input_grad(name, *ts):
+    for t in ts:
+        if t is not None and t.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError(
+                f"hashnerf_amd.{name}: gradients w.r.t. sample positions/directions are not "
+                "implemented (the reference path never needs them: rays carry no grad)")
+
+
+# --------------------------------------------------------------------------
+# hash encoding (embedding/hash_encoding.py:84-110)
+# --------------------------------------------------------------------------
+class HashEncodeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, table: torch.Tensor, grid: L.HnGrid):
+        L.require_device(x, table)
+        x = x.contiguous()
+        n = x.shape[0]
+        n_feat = grid.n_levels * grid.n_features
+        feat = torch.empty((n, n_feat), dtype=torch.float32, device=x.device)
+        keep = torch.empty((n,), dtype=torch.uint8, device=x.device)
+        L.check(L.lib().hn_encode_fwd(grid, L.ptr(x), n, L.ptr(table.contiguous()), L.ptr(feat),
+                                      L.ptr(keep), L.stream(x.device)), "encode_fwd")
+        ctx.save_for_backward(x)
+        ctx.grid = grid
+        ctx.table_shape = table.shape
+        ctx.mark_non_differentiable(keep)
+        return feat, keep.bool()
+
+    @staticmethod
+    def backward(ctx, dfeat, _dkeep):
+        (x,) = ctx.saved_tensors
+        dtable = torch.zeros(ctx.table_shape, dtype=torch.float32, device=x.device)
+        if dfeat is not None:
+            dfeat = dfeat.contiguous()
+            L.check(L.lib().hn_encode_bwd(ctx.grid, L.ptr(x), x.shape[0], L.ptr(dfeat), L.ptr(dtable),
+                                          L.stream(x.device)), "encode_bwd")
+        return None, dtable, None
+
+
+def hash_encode(x, table, grid):
+    _no_input_grad("hash_encode", x)
+    return HashEncodeFn.apply(x, table, grid)
+
+
+def sh_encode(dirs: torch.Tensor) -> torch.Tensor:
+    """SHEncoder.forward, degree 4 (embedding/spherical_harmonic.py:65-103)."""
+    _no_input_grad("sh_encode", dirs)
+    L.require_device(dirs)
+    d = dirs.reshape(-1, 3).contiguous()
+    out = torch.empty((d.shape[0], 16), dtype=torch.float32, device=d.device)
+    L.check(L.lib().hn_sh_fwd(L.ptr(d), d.shape[0], L.ptr(out), L.stream(d.device)), "sh_fwd")
+    return out.reshape(*dirs.shape[:-1], 16)
+
+
+# --------------------------------------------------------------------------
+# NeRFSmall (models.py:151-174)
+# --------------------------------------------------------------------------
+class NeRFSmallFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w0, w1, w2, w3, w4):
+        L.require_device(x, w0, w1, w2, w3, w4)
+        x = x.contiguous()
+        ws = [w.contiguous() for w in (w0, w1, w2, w3, w4)]
+        n = x.shape[0]
+        out = torch.empty((n, 4), dtype=torch.float32, device=x.device)
+        nbytes = L.lib().hn_mlp_workspace_bytes()
+        ws_buf = _ws(nbytes, x.device)
+        L.check(L.lib().hn_mlp_fwd(L.make_mlp(ws), L.ptr(x), n, L.ptr(out), L.ptr(ws_buf), nbytes,
+                                   L.stream(x.device)), "mlp_fwd")
+        ctx.save_for_backward(x, *ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, *ws = ctx.saved_tensors
+        dout = dout.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dws = [torch.zeros_like(w) for w in ws]
+        nbytes = L.lib().hn_mlp_workspace_bytes()
+        ws_buf = _ws(nbytes, x.device)
+        L.check(L.lib().hn_mlp_bwd(L.make_mlp(ws), L.ptr(x), L.ptr(dout), x.shape[0], L.ptr(dx),
+                                   L.make_mlp_grad(dws), L.ptr(ws_buf), nbytes, L.stream(x.device)),
+                "mlp_bwd")
+        return (dx, *dws)
+
+
+# --------------------------------------------------------------------------
+# raw2outputs (run_nerf_helpers.py:577-628) and sample_pdf (:264-307)
+# --------------------------------------------------------------------------
+class CompositeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw, z, rays_d, noise, white: bool):
+        L.require_device(raw, z, rays_d, noise)
+        raw, z, rays_d, noise = (L.contig(t) for t in (raw, z, rays_d, noise))
+        B, S = z.shape
+        dev = raw.device
+        rgb = torch.empty((B, 3), device=dev)
+        disp, acc, depth, ent = (torch.empty((B,), device=dev) for _ in range(4))
+        weights = torch.empty((B, S), device=dev)
+        L.check(L.lib().hn_composite_fwd(L.ptr(raw), L.ptr(z), L.ptr(rays_d), L.ptr(noise), B, S,
+                                         int(white), L.ptr(rgb), L.ptr(disp), L.ptr(acc),
+                                         L.ptr(weights), L.ptr(depth), L.ptr(ent), L.stream(dev)),
+                "composite_fwd")
+        ctx.save_for_backward(raw, z, rays_d, noise, depth)
+        ctx.set_materialize_grads(False)   # unused outputs => NULL, not zeros (0*inf)
+        ctx.white = white
+        return rgb, disp, acc, weights, depth, ent
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_disp, g_acc, g_weights, g_depth, g_ent):
+        raw, z, rays_d, noise, depth = ctx.saved_tensors
+        if g_disp is not None:
+            # disp = 1 / max(1e-10, depth): fold into the depth gradient
+            gd = torch.where(depth > 1e-10, -g_disp / (depth * depth), torch.zeros_like(depth))
+            g_depth = gd if g_depth is None else g_depth + gd
+        B, S = z.shape
+        d_raw = torch.empty_like(raw)
+        L.check(L.lib().hn_composite_bwd(L.ptr(raw), L.ptr(z), L.ptr(rays_d), L.ptr(noise), B, S,
+                                         int(ctx.white), L.ptr(L.contig(g_rgb)), L.ptr(L.contig(g_acc)),
+                                         L.ptr(L.contig(g_depth)), L.ptr(L.contig(g_ent)),
+                                         L.ptr(L.contig(g_weights)), L.ptr(d_raw), L.stream(raw.device)),
+                "composite_bwd")
+        return d_raw, None, None, None, None
+
+
+def sample_pdf(bins: torch.Tensor, weights: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    L.require_device(bins, weights, u)
+    bins, weights, u = bins.contiguous(), weights.detach().contiguous(), u.contiguous()
+    B, nb = bins.shape
+    ns = u.shape[-1]
+    out = torch.empty((B, ns), device=bins.device)
+    L.check(L.lib().hn_sample_pdf(L.ptr(bins), L.ptr(weights), L.ptr(u), B, nb, ns, L.ptr(out),
+                                  L.stream(bins.device)), "sample_pdf")
+    return out
+
+
+# --------------------------------------------------------------------------
+# fused render_rays (run_nerf_helpers.py:464-574)
+# --------------------------------------------------------------------------
+class RenderRaysFn(torch.autograd.Function):
+    """Inputs: rays [B,11], t_vals [64], t_rand [B,64]|None, u [B,128],
+    noise_c/noise_f |None, table, 5 coarse + 5 fine NeRFSmall weights.
+    Outputs: rgb, depth, acc, sparsity, rgb0, depth0, acc0, sparsity0, z_std, raw."""
+
+    @staticmethod
+    def forward(ctx, cfg: L.HnRenderCfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws):
+        L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
+        rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
+                                                                          noise_c, noise_f))
+        ws = [w.contiguous() for w in ws]
+        B = rays.shape[0]
+        dev = rays.device
+        e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)
+        out = dict(rgb=e(B, 3), depth=e(B), acc=e(B), sparsity=e(B), rgb0=e(B, 3), depth0=e(B),
+                   acc0=e(B), sparsity0=e(B), z_std=e(B), z_coarse=e(B, 64), z_fine=e(B, 192),
+                   raw_c=e(B, 64, 4), raw_f=e(B, 192, 4))
+        a = L.HnRenderFwdArgs()
+        a.n_rays = B
+        for k, t in (("rays", rays), ("t_vals", t_vals), ("t_rand", t_rand), ("u", u),
+                     ("noise_c", noise_c), ("noise_f", noise_f), ("table", table)):
+            setattr(a, k, None if t is None else t.data_ptr())
+        a.coarse = L.make_mlp(ws[:5])
+        a.fine = L.make_mlp(ws[5:])
+        for k, t in out.items():
+            setattr(a, k, t.data_ptr())
+        nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
+        wsb = _ws(nbytes, dev)
+        L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
+        ctx.cfg = cfg
+        ctx.set_materialize_grads(False)   # unused outputs => NULL, not zeros (0*inf)
+        ctx.has_noise = (noise_c is not None, noise_f is not None)
+        ctx.save_for_backward(rays, noise_c if noise_c is not None else rays,
+                              noise_f if noise_f is not None else rays, table, out["z_coarse"],
+                              out["z_fine"], out["raw_c"], out["raw_f"], *ws)
+        ctx.mark_non_differentiable(out["z_std"])
+        return (out["rgb"], out["depth"], out["acc"], out["sparsity"], out["rgb0"], out["depth0"],
+                out["acc0"], out["sparsity0"], out["z_std"], out["raw_f"])
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_acc, g_sp, g_rgb0, g_depth0, g_acc0, g_sp0, _g_zstd, g_raw):
+        rays, noise_c, noise_f, table, z_c, z_f, raw_c, raw_f, *ws = ctx.saved_tensors
+        noise_c = noise_c if ctx.has_noise[0] else None
+        noise_f = noise_f if ctx.has_noise[1] else None
+        B = rays.shape[0]
+        dev = rays.device
+        d_table = torch.zeros_like(table)
+        dws = [torch.zeros_like(w) for w in ws]
+        a = L.HnRenderBwdArgs()
+        a.n_rays = B
+        a.coarse = L.make_mlp(ws[:5])
+        a.fine = L.make_mlp(ws[5:])
+        grads = dict(g_rgb=g_rgb, g_depth=g_depth, g_acc=g_acc, g_sparsity=g_sp, g_rgb0=g_rgb0,
+                     g_depth0=g_depth0, g_acc0=g_acc0, g_sparsity0=g_sp0, g_raw_f=g_raw)
+        keep = []
+        for k, t in list(grads.items()) + [("rays", rays), ("noise_c", noise_c), ("noise_f", noise_f),
+                                           ("table", table), ("z_coarse", z_c), ("z_fine", z_f),
+                                           ("raw_c", raw_c), ("raw_f", raw_f), ("d_table", d_table)]:
+            t = L.contig(t)
+            keep.append(t)
+            setattr(a, k, None if t is None else t.data_ptr())
+        a.d_coarse = L.make_mlp_grad(dws[:5])
+        a.d_fine = L.make_mlp_grad(dws[5:])
+        nbytes = L.lib().hn_render_workspace_bytes(ctx.cfg, B)
+        wsb = _ws(nbytes, dev)
+        L.check(L.lib().hn_render_bwd(ctx.cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_bwd")
+        return (None, None, None, None, None, None, None, d_table, *dws)
+
+
+def make_render_cfg(grid: L.HnGrid, white_bkgd: bool, lindisp: bool, perturb: bool,
+                    n_samples: int = 64, n_importance: int = 128) -> L.HnRenderCfg:
+    c = L.HnRenderCfg()
+    c.grid = grid
+    c.n_samples, c.n_importance = n_samples, n_importance
+    c.white_bkgd, c.lindisp, c.perturb = int(white_bkgd), int(lindisp), int(perturb)
+    return c
+
+
+def render_rays_fused(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table,
+                      coarse_ws: Sequence[torch.Tensor], fine_ws: Sequence[torch.Tensor]):
+    return RenderRaysFn.apply(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table,
+                              *coarse_ws, *fine_ws)

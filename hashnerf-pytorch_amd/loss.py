@@ -1,0 +1,51 @@
+"""Losses of the training step: hash-table total variation (loss.py:11-43) and
+the run_nerf.py:612-636 loss assembly."""
+from __future__ import annotations
+
+from math import exp, floor, log
+
+import torch
+
+from .embedding import hash as spatial_hash
+
+
+def tv_cube(level, n_levels, min_resolution, max_resolution):
+    """Resolution and cube edge of loss.py:13-22 (float64 math, floor, clip)."""
+    b = exp((log(max_resolution) - log(min_resolution)) / (n_levels - 1))
+    resolution = torch.tensor(floor(min_resolution * b ** level))
+    min_cube, max_cube = min_resolution - 1, 50
+    if min_cube > max_cube:
+        raise ValueError("total_variation_loss: min cuboid size greater than max")
+    cube = torch.floor(torch.clip(resolution / 10.0, min_cube, max_cube)).int()
+    return resolution, cube
+
+
+def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2_hashmap_size,
+                         n_levels=16, min_vertex=None, generator=None):
+    """loss.py:11-43.  ``embeddings`` is ``HashEmbedder.embeddings[level]``;
+    ``min_vertex`` (3 ints) replaces the torch.randint draw (:25) when given."""
+    min_resolution = int(min_resolution)
+    max_resolution = int(max_resolution)
+    resolution, cube = tv_cube(level, n_levels, min_resolution, max_resolution)
+    if min_vertex is None:
+        min_vertex = torch.randint(0, int(resolution - cube), (3,), generator=generator)
+    dev = embeddings.weight.device
+    idx = min_vertex.to(dev) + torch.stack([torch.arange(int(cube) + 1, device=dev)] * 3, -1)
+    cube_idx = torch.stack(torch.meshgrid(idx[:, 0], idx[:, 1], idx[:, 2], indexing="ij"), -1)
+    e = embeddings(spatial_hash(cube_idx, log2_hashmap_size))
+    tv_x = torch.pow(e[1:] - e[:-1], 2).sum()
+    tv_y = torch.pow(e[:, 1:] - e[:, :-1], 2).sum()
+    tv_z = torch.pow(e[:, :, 1:] - e[:, :, :-1], 2).sum()
+    return (tv_x + tv_y + tv_z) / cube.to(dev)
+
+
+def training_loss(rgb, extras, target, sparse_loss_weight=1e-10):
+    """run_nerf.py:612-623: mse(rgb) + mse(rgb0) + w * (sum H + sum H0)."""
+    img_loss = torch.mean((rgb - target) ** 2)
+    loss = img_loss
+    if "rgb0" in extras:
+        loss = loss + torch.mean((extras["rgb0"] - target) ** 2)
+    sp = extras["sparsity_loss"].sum()
+    if "sparsity_loss0" in extras:
+        sp = sp + extras["sparsity_loss0"].sum()
+    return loss + sparse_loss_weight * sp, img_loss

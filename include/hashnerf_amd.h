@@ -1,0 +1,179 @@
+/*
+ * hashnerf_amd.h -- C ABI of the MI355X (gfx950) HashNeRF hot path.
+ *
+ * Plain pointers + sizes, no torch types.  Every pointer is a DEVICE pointer
+ * (HBM, fp32, contiguous, row-major) unless documented otherwise; config
+ * structs are HOST pointers read at call time.  `stream` is a hipStream_t
+ * passed as void*.  The library never allocates, frees or synchronises:
+ * scratch comes in through `workspace`; outputs are caller-allocated.
+ * Gradient outputs named d* are ACCUMULATED (+=) so the caller zeroes them,
+ * mirroring autograd's .grad accumulation.  Return value: 0 on success,
+ * a positive HN_E_* code for argument errors, or a hipError_t + 1000.
+ *
+ * Each entry point cites the reference interface it replaces
+ * (mache102/HashNeRF-pytorch, file:line).
+ */
+#ifndef HASHNERF_AMD_H
+#define HASHNERF_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HN_ABI_VERSION 1
+#define HN_MAX_LEVELS 32
+
+enum {
+  HN_OK = 0,
+  HN_E_NULL = 1,        /* required pointer is NULL */
+  HN_E_SHAPE = 2,       /* unsupported size (e.g. n_levels, n_samples) */
+  HN_E_WORKSPACE = 3,   /* workspace too small */
+  HN_E_HIP = 1000       /* + hipError_t */
+};
+
+/* Hash-grid description (embedding/hash_encoding.py:14-57).  grid_size is
+ * (box_max - box_min) / resolution_l evaluated on the host in fp32 exactly as
+ * hash_encoding.py:72/:101 do, so the device sees bit-identical cell sizes.
+ * Table layout in HBM: [n_levels][2^log2_hashmap_size][n_features] fp32
+ * (the stacked `embeddings.{l}.weight` tensors). */
+typedef struct hn_grid {
+  int32_t n_levels;            /* L <= HN_MAX_LEVELS (16) */
+  int32_t n_features;          /* F, must be 2 */
+  int32_t log2_hashmap_size;   /* T, 1..24 */
+  int32_t reserved;
+  float box_min[3];
+  float box_max[3];
+  float grid_size[HN_MAX_LEVELS][3];
+} hn_grid;
+
+/* NeRFSmall weights (models.py:96-149; num_layers=2, hidden 64, geo 15,
+ * num_layers_color=3): torch nn.Linear layout [out][in], no biases. */
+typedef struct hn_mlp {
+  const float* sigma0;   /* sigma_net.0.weight [64][32] */
+  const float* sigma1;   /* sigma_net.1.weight [16][64] */
+  const float* color0;   /* color_net.0.weight [64][31]  (in = [sh16 | geo15]) */
+  const float* color1;   /* color_net.1.weight [64][64] */
+  const float* color2;   /* color_net.2.weight [3][64] */
+} hn_mlp;
+
+typedef struct hn_mlp_grad {
+  float* sigma0; float* sigma1; float* color0; float* color1; float* color2;  /* += */
+} hn_mlp_grad;
+
+#define HN_MLP_PARAMS 9344          /* 2048 + 1024 + 1984 + 4096 + 192 */
+#define HN_MLP_PACKED_FLOATS 24064  /* MFMA fragment-ordered copy, per net */
+
+int32_t hn_abi_version(void);
+const char* hn_status_string(int32_t status);
+
+/* ---- L1 encodings --------------------------------------------------------
+ * HashEmbedder.forward (hash_encoding.py:84-110): x[n][3] -> feat[n][L*F],
+ * keep_mask[n] (uint8, may be NULL).  Corners from the clamped point, trilinear
+ * weights from the unclamped point, every level hashed (SURVEY 8a traps 1-3). */
+int32_t hn_encode_fwd(const hn_grid* g, const float* x, int64_t n, const float* table,
+                      float* feat, uint8_t* keep_mask, void* stream);
+/* Autograd of the above (embedding_dense_backward x L): dtable += scatter. */
+int32_t hn_encode_bwd(const hn_grid* g, const float* x, int64_t n, const float* dfeat,
+                      float* dtable, void* stream);
+/* SHEncoder.forward, degree 4 (embedding/spherical_harmonic.py:65-103):
+ * dirs[n][3] -> out[n][16]. */
+int32_t hn_sh_fwd(const float* dirs, int64_t n, float* out, void* stream);
+
+/* ---- L2 NeRFSmall (MFMA) ------------------------------------------------
+ * NeRFSmall.forward (models.py:151-174): x[n][48] = [feat32 | sh16] ->
+ * out[n][4] = [rgb3 | sigma].  workspace >= hn_mlp_workspace_bytes(). */
+size_t hn_mlp_workspace_bytes(void);
+int32_t hn_mlp_fwd(const hn_mlp* w, const float* x, int64_t n, float* out,
+                   void* workspace, size_t ws_bytes, void* stream);
+/* Backward: dx[n][48] (overwritten; may be NULL), dw (+=). */
+int32_t hn_mlp_bwd(const hn_mlp* w, const float* x, const float* dout, int64_t n,
+                   float* dx, const hn_mlp_grad* dw, void* workspace, size_t ws_bytes,
+                   void* stream);
+
+/* ---- L3 volume rendering --------------------------------------------------
+ * raw2outputs (run_nerf_helpers.py:577-628), n_samples <= 256 per ray:
+ * raw[n_rays][S][4], z[n_rays][S], rays_d[n_rays][3], noise[n_rays][S] or NULL
+ * -> rgb[n_rays][3], disp, acc, depth, entropy [n_rays], weights[n_rays][S]. */
+int32_t hn_composite_fwd(const float* raw, const float* z, const float* rays_d,
+                         const float* noise, int64_t n_rays, int32_t n_samples,
+                         int32_t white_bkgd, float* rgb, float* disp, float* acc,
+                         float* weights, float* depth, float* entropy, void* stream);
+/* Backward w.r.t. raw (overwritten): upstream grads of rgb[n][3], acc[n],
+ * depth[n], entropy[n], weights[n][S] (any may be NULL = 0). */
+int32_t hn_composite_bwd(const float* raw, const float* z, const float* rays_d,
+                         const float* noise, int64_t n_rays, int32_t n_samples,
+                         int32_t white_bkgd, const float* g_rgb, const float* g_acc,
+                         const float* g_depth, const float* g_entropy,
+                         const float* g_weights, float* d_raw, void* stream);
+/* sample_pdf (run_nerf_helpers.py:264-307) with u given:
+ * bins[n_rays][nb], weights[n_rays][nb-1], u[n_rays][ns] -> out[n_rays][ns];
+ * nb <= 256. */
+int32_t hn_sample_pdf(const float* bins, const float* weights, const float* u,
+                      int64_t n_rays, int32_t n_bins, int32_t n_samples, float* out,
+                      void* stream);
+
+/* ---- fused render_rays (run_nerf_helpers.py:464-574) ---------------------
+ * One kernel for the whole forward of a ray batch (coarse 64 -> composite ->
+ * sample_pdf 128 -> sort -> fine 192 -> composite) and one for its backward.
+ * Hash grid must have L=16, F=2; N_samples=64, N_importance=128. */
+typedef struct hn_render_cfg {
+  hn_grid grid;
+  int32_t n_samples;      /* 64 */
+  int32_t n_importance;   /* 128 */
+  int32_t white_bkgd;
+  int32_t lindisp;
+  int32_t perturb;        /* 1: stratified jitter from t_rand */
+  int32_t reserved[3];
+} hn_render_cfg;
+
+typedef struct hn_render_fwd_args {
+  int64_t n_rays;
+  const float* rays;        /* [B][11] = [o3 d3 near far viewdir3] (run_nerf_helpers.py:509-512) */
+  const float* t_vals;      /* [64]   torch.linspace(0,1,64) (:514) */
+  const float* t_rand;      /* [B][64] jitter (:528) or NULL if !perturb */
+  const float* u;           /* [B][128] importance uniforms (:276) */
+  const float* noise_c;     /* [B][64] or NULL (raw_noise_std = 0) */
+  const float* noise_f;     /* [B][192] or NULL */
+  const float* table;       /* [16][2^T][2] */
+  hn_mlp coarse;            /* network_fn */
+  hn_mlp fine;              /* network_fine */
+  /* outputs (render_rays ret, :560-568) */
+  float* rgb; float* depth; float* acc; float* sparsity;        /* fine: [B][3],[B],[B],[B] */
+  float* rgb0; float* depth0; float* acc0; float* sparsity0;    /* coarse */
+  float* z_std;             /* [B] */
+  /* saved for backward (also returned: raw = raw_f) */
+  float* z_coarse;          /* [B][64] */
+  float* z_fine;            /* [B][192] */
+  float* raw_c;             /* [B][64][4] */
+  float* raw_f;             /* [B][192][4] */
+} hn_render_fwd_args;
+
+typedef struct hn_render_bwd_args {
+  int64_t n_rays;
+  const float* rays;
+  const float* noise_c; const float* noise_f;
+  const float* table;
+  hn_mlp coarse; hn_mlp fine;
+  const float* z_coarse; const float* z_fine; const float* raw_c; const float* raw_f;
+  /* upstream grads (NULL = 0) */
+  const float* g_rgb; const float* g_depth; const float* g_acc; const float* g_sparsity;
+  const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;
+  const float* g_raw_f;     /* [B][192][4] or NULL */
+  /* gradient outputs (+=) */
+  float* d_table;           /* [16][2^T][2] */
+  hn_mlp_grad d_coarse; hn_mlp_grad d_fine;
+} hn_render_bwd_args;
+
+size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
+int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
+                      void* workspace, size_t ws_bytes, void* stream);
+int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_args* a,
+                      void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HASHNERF_AMD_H */

@@ -1,0 +1,89 @@
+"""CPU-side checks of the C ABI boundary: the library loads without a GPU, it
+exports every symbol include/hashnerf_amd.h declares, the ctypes struct
+layouts match the header, and argument validation fails loudly (no compute
+call is made)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "hashnerf_amd.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|size_t|const char\*)\s+(hn_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol(hn):
+    lib = hn._lib.lib()
+    names = declared_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
+    assert lib.hn_abi_version() == 1
+
+
+def test_struct_sizes_match_header(hn):
+    L = hn._lib
+    assert C.sizeof(L.HnGrid) == 16 + 24 + 32 * 12
+    assert C.sizeof(L.HnMlp) == 5 * 8
+    assert C.sizeof(L.HnRenderCfg) == C.sizeof(L.HnGrid) + 8 * 4
+    assert L.lib().hn_mlp_workspace_bytes() == L.MLP_PACKED_FLOATS * 4
+
+
+def test_argument_validation_without_gpu(hn):
+    L = hn._lib
+    lib = L.lib()
+    g = L.make_grid(16, 2, 19, [-1] * 3, [1] * 3, [[0.1] * 3] * 16)
+    # n == 0 is a no-op; NULL pointers and bad shapes are rejected before any launch
+    assert lib.hn_encode_fwd(g, None, 0, None, None, None, None) == 0
+    assert lib.hn_encode_fwd(g, None, 10, None, None, None, None) == 1
+    g.n_features = 4
+    assert lib.hn_encode_fwd(g, None, 10, None, None, None, None) == 2
+    assert lib.hn_sample_pdf(None, None, None, 4, 300, 8, None, None) == 2
+    cfg = L.HnRenderCfg()
+    cfg.grid = L.make_grid(8, 2, 19, [-1] * 3, [1] * 3, [[0.1] * 3] * 8)
+    a = L.HnRenderFwdArgs()
+    a.n_rays = 4
+    assert lib.hn_render_fwd(cfg, a, None, 0, None) == 2   # L != 16
+    assert lib.hn_status_string(3).decode() == "workspace too small"
+
+
+def test_product_path_refuses_cpu_tensors(hn):
+    emb = hn.HashEmbedder((torch.tensor([-1., -1, -1]), torch.tensor([1., 1, 1])), log2_hashmap_size=12)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        emb(torch.zeros(4, 3))
+    with pytest.raises(RuntimeError, match="ROCm"):
+        hn.SHEncoder()(torch.zeros(4, 3))
+
+
+def test_state_dict_round_trip_reference_keys(hn, oracle):
+    emb = hn.HashEmbedder((torch.tensor([-1., -1, -1]), torch.tensor([1., 1, 1])), log2_hashmap_size=10)
+    sd = emb.state_dict()
+    assert list(sd) == [f"embeddings.{l}.weight" for l in range(16)]
+    assert sd["embeddings.3.weight"].shape == (1024, 2)
+    emb2 = hn.HashEmbedder((torch.tensor([-1., -1, -1]), torch.tensor([1., 1, 1])), log2_hashmap_size=10)
+    emb2.load_state_dict(sd)
+    assert torch.equal(emb2.table, emb.table)
+    # the level views behave like nn.Embedding (used by the TV loss)
+    idx = torch.tensor([0, 5, 1023])
+    assert torch.equal(emb.embeddings[3](idx), emb.table[3][idx])
+
+
+def test_grid_sizes_bitexact_with_reference_formula(hn, oracle):
+    box = (torch.tensor([-4.0249, -4.0249, -3.3366]), torch.tensor([4.0249, 4.0249, 3.2414]))
+    for finest in (512, 1024):
+        emb = hn.HashEmbedder(box, log2_hashmap_size=12, finest_resolution=finest)
+        res = oracle.level_resolutions(16, 16, finest)
+        assert [float(r) for r in emb.resolutions] == [float(r) for r in res]
+        gs = oracle.grid_sizes(box[0], box[1], res)
+        g = emb.grid()
+        for l in range(16):
+            for a in range(3):
+                assert C.c_float(gs[l, a].item()).value == g.grid_size[l][a]
