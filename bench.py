@@ -1,0 +1,188 @@
+"""Headline benchmark: training rays/s (fwd+bwd) of the HashNeRF step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+
+N = 1 runs BASELINE.json configs[1] (chair, N_rand 4096, 64+128 samples,
+L=16 F=2 T=2^19 finest 512) on one MI355X.  N > 1 is launched by torchrun
+(one process per GPU, RCCL): data-parallel over rays, per-rank N_rand fixed
+(weak scaling), one SUM all-reduce of hash + MLP grads per step.
+
+A step is one full training iteration: on-device ray sampling from a
+synthetic 400x400 image set resident in HBM, fused render forward, loss
+(MSE fine+coarse, entropy sparsity, TV), fused backward, gradient
+all-reduce (N > 1), RAdam step, lr decay.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    2: dict(workload="chair 1xMI355X N_rand=4096 64+128 L16 F2 T19 finest512 (BASELINE configs[1])",
+            N_rand=4096, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6),
+    3: dict(workload="lego T22 finest1024 N_rand=8192 TV on (BASELINE configs[2])",
+            N_rand=8192, log2_hashmap_size=22, finest_res=1024, tv_loss_weight=1e-6),
+    4: dict(workload="hotdog DP, N_rand=8192 per GPU (BASELINE configs[3])",
+            N_rand=8192, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6),
+}
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+PT_BYTES = 16 * 8 * 8          # one point: 16 levels x 8 corners x (2 x fp32)
+UNIQUE_PTS = 192               # per ray (the 64 coarse points recur in the fine pass)
+# per ray 192 unique points gathered + scatter-added, + 36 B ray I/O
+PATH_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2 + 36
+BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2        # bwd kernel: re-gather + scatter-add
+FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
+
+
+def cpu_baseline(cfg, seconds=12.0, n_rays=256):
+    """Oracle (torch-CPU restatement of the reference) training step on a
+    bounded sample of the same workload: n_rays rays of the same scene shape,
+    same table size, fwd + bwd + RAdam; rays/s over >= 2 timed steps."""
+    import numpy as np
+
+    from oracle import hashnerf_oracle as O
+
+    threads = torch.get_num_threads()
+    T, finest = cfg["log2_hashmap_size"], cfg["finest_res"]
+    g = torch.Generator().manual_seed(0)
+    box = (torch.tensor([-4.02, -4.02, -3.34]), torch.tensor([4.02, 4.02, 3.24]))
+    tab = ((torch.rand(16, 2 ** T, 2, generator=g) * 2 - 1) * 1e-4).requires_grad_(True)
+    wc = {k: v.requires_grad_(True) for k, v in O.init_nerf_small(g).items()}
+    wf = {k: v.requires_grad_(True) for k, v in O.init_nerf_small(g).items()}
+    params = [tab] + list(wc.values()) + list(wf.values())
+    state = [(torch.zeros_like(p), torch.zeros_like(p)) for p in params]
+    res = O.level_resolutions(16, 16, finest)
+    H = W = 400
+    focal = .5 * W / np.tan(.5 * 0.6911112070083618)
+    K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])
+
+    def step(i):
+        c2w = O.pose_spherical(float(i * 37 % 360 - 180), -30.0, 4.0)
+        ro, rd = O.get_rays(H, W, K, c2w[:3, :4])
+        sel = torch.randperm(H * W, generator=g)[:n_rays]
+        ro, rd = ro.reshape(-1, 3)[sel], rd.reshape(-1, 3)[sel]
+        vd = rd / torch.norm(rd, dim=-1, keepdim=True)
+        rb = torch.cat([ro, rd, 2 * torch.ones(n_rays, 1), 6 * torch.ones(n_rays, 1), vd], -1)
+        ret = O.render_rays(rb, wc, wf, tab, box[0], box[1], res, T,
+                            t_rand=torch.rand(n_rays, 64, generator=g),
+                            u=torch.rand(n_rays, 128, generator=g), white_bkgd=True)
+        loss = O.training_loss(ret, torch.rand(n_rays, 3, generator=g), 1e-10)
+        for p in params:
+            p.grad = None
+        loss.backward()
+        with torch.no_grad():
+            for p, (m, v) in zip(params, state):
+                O.radam_step(p, p.grad, m, v, i + 1, 0.01, weight_decay=1e-6 if p is not tab else 0.0,
+                             eps=1e-15 if p is tab else 1e-8)
+
+    step(0)                                   # warm-up
+    t0 = time.perf_counter()
+    n = 0
+    while n < 2 or (time.perf_counter() - t0 < seconds and n < 20):
+        step(n + 1)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * n_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{n} oracle training steps x {n_rays} rays (T=2^{T}, finest {finest}, 64+128, "
+                      f"fwd+bwd+RAdam) on {threads} host threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=None)
+    ap.add_argument("--n-rand", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg_id = args.config or (2 if world == 1 else 4)
+    cfg = dict(CONFIGS[cfg_id])
+    if args.n_rand:
+        cfg["N_rand"] = args.n_rand
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import hn_loader
+    hn = hn_loader.load()
+    from hashnerf_pytorch_amd import functional as HF
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+
+    targs = default_args(N_rand=cfg["N_rand"], log2_hashmap_size=cfg["log2_hashmap_size"],
+                         finest_res=cfg["finest_res"], tv_loss_weight=cfg["tv_loss_weight"],
+                         tv_until=10 ** 9)
+    data = SyntheticBlender(400, 400, 100, dev, seed=0)
+    tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0)
+
+    for i in range(args.warmup):
+        tr.step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    HF.TIMER.reset()
+    HF.TIMER.enabled = True
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        loss, mse = tr.step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    HF.TIMER.enabled = False
+    t = torch.tensor([dt], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    fwd_ms = HF.TIMER.mean_ms("render_fwd")
+    bwd_ms = HF.TIMER.mean_ms("render_bwd")
+    B = cfg["N_rand"]
+    value = world * B * args.steps / dt
+    if rank == 0:
+        bwd_gbs = B * BWD_BYTES_PER_RAY / (bwd_ms * 1e-3) / 1e9
+        fwd_gbs = B * FWD_BYTES_PER_RAY / (fwd_ms * 1e-3) / 1e9
+        line = {
+            "metric": "training rays/sec (fwd+bwd) on chair; PSNR@5k iters",
+            "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (procedural 400x400 blender-style cameras, uniform targets)",
+            "config": {"workload": cfg["workload"], "rays_per_gpu": B, "global_batch": B * world,
+                       "samples_per_ray": "64+128", "log2_hashmap_size": cfg["log2_hashmap_size"],
+                       "finest_res": cfg["finest_res"], "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "kernel": "render_bwd (hn_render_bwd launch)",
+                         "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(bwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_ray": BWD_BYTES_PER_RAY, "launch_ms": round(bwd_ms, 4)},
+            "kernels": {"render_fwd_ms": round(fwd_ms, 4), "render_fwd_GBs": round(fwd_gbs, 1),
+                        "render_bwd_ms": round(bwd_ms, 4),
+                        "path_GBs": round(value / world * PATH_BYTES_PER_RAY / 1e9, 1),
+                        "path_frac": round(value / world * PATH_BYTES_PER_RAY / 1e9 / HBM_PEAK_GBS, 4)},
+            "loss": round(float(loss.item()), 6),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, seconds=args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -14,7 +14,7 @@ from typing import Optional
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libhashnerf_amd.so")
+LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 24064

@@ -33,6 +33,19 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
+def build_variant(defines, out_lib, verbose=False) -> str:
+    """Diagnostic build (e.g. ``["-DHN_ABLATE=1"]``) into its own .so and objects."""
+    objdir = out_lib + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for src in sources():
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
+        subprocess.run([HIPCC, *CFLAGS, *defines, "-c", src, "-o", obj], check=True)
+        objs.append(obj)
+    subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", *objs, "-o", out_lib], check=True)
+    return out_lib
+
+
 def build(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(OBJDIR, exist_ok=True)

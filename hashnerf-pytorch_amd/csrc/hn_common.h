@@ -77,6 +77,31 @@ HN_DEV void voxel_level(const float x[3], const float xc[3], const float gs[3],
   v.h[7] = (x1 ^ y1 ^ z1) & mask;
 }
 
+// voxel_level that also returns the integer cell (run detection along rays).
+HN_DEV void voxel_level_cell(const float x[3], const float xc[3], const float gs[3],
+                             const float bmin[3], uint32_t mask, Voxel& v, uint32_t cell[3]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float q = (xc[a] - bmin[a]) / gs[a];
+    const int32_t i = (int32_t)floorf(q);
+    const float vmin = (float)i * gs[a] + bmin[a];
+    const float vmax = vmin + gs[a];
+    v.w[a] = (x[a] - vmin) / (vmax - vmin);
+    cell[a] = (uint32_t)i;
+  }
+  const uint32_t x0 = cell[0], x1 = cell[0] + 1u;
+  const uint32_t y0 = cell[1] * kPrimeY, y1 = (cell[1] + 1u) * kPrimeY;
+  const uint32_t z0 = cell[2] * kPrimeZ, z1 = (cell[2] + 1u) * kPrimeZ;
+  v.h[0] = (x0 ^ y0 ^ z0) & mask;
+  v.h[1] = (x0 ^ y0 ^ z1) & mask;
+  v.h[2] = (x0 ^ y1 ^ z0) & mask;
+  v.h[3] = (x0 ^ y1 ^ z1) & mask;
+  v.h[4] = (x1 ^ y0 ^ z0) & mask;
+  v.h[5] = (x1 ^ y0 ^ z1) & mask;
+  v.h[6] = (x1 ^ y1 ^ z0) & mask;
+  v.h[7] = (x1 ^ y1 ^ z1) & mask;
+}
+
 // trilinear_interp (hash_encoding.py:130-163): x first, then y, then z.
 HN_DEV float trilerp(const float e[8], const float w[3]) {
   const float ax = 1.f - w[0], ay = 1.f - w[1], az = 1.f - w[2];

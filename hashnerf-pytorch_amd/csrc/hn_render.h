@@ -225,20 +225,64 @@ HN_DEV void composite_bwd(const float* raw, const float* z, const float* noise, 
   }
 }
 
+// torch.sum over a contiguous fp32 row on the CPU (ATen SumKernel.cpp
+// vectorized_inner_sum: 8-float vectors, row_sum with 4-way ILP, scalar tail,
+// then the 8 vector lanes) restated for n < 512, so that
+// `weights / torch.sum(weights)` (run_nerf_helpers.py:267) is bit-identical.
+// Every lane evaluates it redundantly from LDS (broadcast reads).
+HN_DEV float torch_row_sum(const float* x, int n) {
+  const int nv = n >> 3;
+  float acc[8];
+  if (nv >= 4) {
+    const int size_ilp = nv >> 2;
+    float p[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) p[k][l] = 0.f;
+    for (int i = 0; i < size_ilp; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) p[k][l] += x[(i * 4 + k) * 8 + l];
+    for (int i = size_ilp * 4; i < nv; ++i)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) p[0][l] += x[i * 8 + l];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) p[0][l] += p[k][l];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[l] = p[0][l];
+  } else {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[l] = 0.f;
+    for (int i = 0; i < nv; ++i)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) acc[l] += x[i * 8 + l];
+  }
+  float fin = 0.f;
+  for (int k = nv * 8; k < n; ++k) fin += x[k];
+#pragma unroll
+  for (int l = 0; l < 8; ++l) fin += acc[l];
+  return fin;
+}
+
 // sample_pdf for one ray.  bins[nw+1], w[nw] (any memory), cdf: LDS scratch
 // [nw+1], u[ns] (global), out[ns].  nw + 1 <= 256.
 HN_DEV void sample_pdf_wave(const float* bins, const float* w, int nw, float* cdf_lds,
                             const float* u, int ns, float* out, int lane) {
   constexpr int NPL = 4;                       // weights per lane (nw <= 255)
   float wp[NPL];
-  double s = 0;
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
     const int j = lane * NPL + k;
     wp[k] = j < nw ? w[j] + 1e-5f : 0.f;      // weights + 1e-5 (:266)
-    s += (double)wp[k];
+    if (j < nw) cdf_lds[j + 1] = wp[k];       // staged for the row sum
   }
-  const float sum = (float)wave_sum(s);
+  lds_fence_wave();
+  const float sum = torch_row_sum(cdf_lds + 1, nw);
+  lds_fence_wave();
   double pd[NPL], loc = 0;
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {

@@ -15,6 +15,12 @@
 #include "hn_mlp.h"
 #include "hn_render.h"
 
+// Diagnostic ablations (never set in the product build): 1 = no scatter
+// atomics, 2 = no MLP in the backward (gather + scatter only).
+#ifndef HN_ABLATE
+#define HN_ABLATE 0
+#endif
+
 namespace hn {
 
 constexpr int kSc = 64, kNi = 128, kSf = 192;
@@ -103,27 +109,68 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
   }
 }
 
-// Trilinear backward + scatter-add of one point's 16 feature grads into the
-// table gradient (embedding_dense_backward of hash_encoding.py:106).
+// One level of the scatter for the 32 points of a tile (lane half h adds
+// feature h; both halves see the same point and level, so the f0/f1 atomics
+// of an entry are two adjacent dwords of ONE wave-instruction = one memory
+// request).  Consecutive lanes are consecutive samples along the ray; a run
+// of samples inside one voxel shares all 8 corners, so the run is summed in
+// registers first (segmented suffix sum over the half-wave) and only its head
+// lane issues the 8 atomics.  The reduction is skipped when the level has no
+// run (fine levels, sparse samples).
+HN_DEV void scatter_level(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
+                          const float pt[3], const float xc[3], uint32_t l, float gf, int p, int h) {
+  const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
+  const uint32_t mask = (1u << g.log2T) - 1u;
+  Voxel v;
+  uint32_t cell[3];
+  voxel_level_cell(pt, xc, gs, g.bmin, mask, v, cell);
+  float cv[8];
+  trilerp_bwd(gf, v.w, cv);
+  const uint32_t q0 = __shfl_up(cell[0], 1, 32), q1 = __shfl_up(cell[1], 1, 32),
+                 q2 = __shfl_up(cell[2], 1, 32);
+  const bool head = p == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
+  const uint32_t hm = (uint32_t)(__ballot(head) >> (32 * h));   // heads of this half
+#pragma unroll
+  for (int d = 1; d < 32; d <<= 1) {
+    // lane p absorbs lane p+d iff no run starts in (p, p+d]
+    const bool same = p + d < 32 && ((hm >> (p + 1)) & ((1u << d) - 1u)) == 0u;
+    if (!__any(same)) break;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float o = __shfl_down(cv[c], d, 32);
+      if (same) cv[c] += o;
+    }
+  }
+  if (head) {
+    const uint32_t row0 = l << g.log2T;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
+                                            (row0 + v.h[c]) * 8u + 4u * h);
+      atomic_add_f32(dst, cv[c]);
+    }
+  }
+}
+
+// Trilinear backward + scatter-add of one tile's feature grads into the table
+// gradient (embedding_dense_backward of hash_encoding.py:106).
 HN_DEV void scatter_tile(const GridArgs& g, const float* gsl, float* __restrict__ dtable, const float pt[3], int h,
                          const f32x16& dfeat) {
+  const int p = lane_id() & 31;
   float xc[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], g.bmin[a], g.bmax[a]);
-  const uint32_t mask = (1u << g.log2T) - 1u;
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    const int l0 = tile_level(m, 0), l1 = tile_level(m, 1);
-    const uint32_t l = h ? l1 : l0;
-    const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
-    Voxel v;
-    voxel_level(pt, xc, gs, g.bmin, mask, v);
-    float c0[8], c1[8];
-    trilerp_bwd(dfeat[2 * m], v.w, c0);
-    trilerp_bwd(dfeat[2 * m + 1], v.w, c1);
-    const uint32_t row0 = l << g.log2T;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) atomic_add_row(dtable, (row0 + v.h[c]) * 8u, c0[c], c1[c]);
+    // lane half h holds (f0, f1) of level tile_level(m, h); trade so that
+    // half h holds feature h of both levels tile_level(m, 0/1)
+    const float g0 = dfeat[2 * m], g1 = dfeat[2 * m + 1];
+    const float recv = __shfl_xor(h ? g0 : g1, 32, 64);
+    const float ga = h ? recv : g0;     // feature h of level tile_level(m, 0)
+    const float gb = h ? g1 : recv;     // feature h of level tile_level(m, 1)
+    scatter_level(g, gsl, dtable, pt, xc, tile_level(m, 0), ga, p, h);
+    __builtin_amdgcn_sched_barrier(0);
+    scatter_level(g, gsl, dtable, pt, xc, tile_level(m, 1), gb, p, h);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -313,15 +360,23 @@ HN_DEV void bwd_ray(const RenderBK& k, int64_t ray, bool fine, float* Wacc, floa
     ray_point(r, zb[q], pt);
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
+    f32x16 dfeat;
+#if HN_ABLATE == 2   // diagnostic build: gather + scatter only (no MLP)
+    dfeat = feat;
+#else
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
     const float4 dr = *reinterpret_cast<const float4*>(rawb + 4 * q);
     const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
     const float rgbg[3] = {dr.x, dr.y, dr.z};
-    f32x16 dfeat;
     mlp_bwd_tile(P, feat, shx8, a, dy2, dr.w, rgbg, T, Wacc, dfeat, nullptr, lane);
+#endif
+#if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
+    if (dfeat[0] == 1234.5f && dfeat[1] == -1234.5f) k.d_table[lane] = dfeat[2];
+#else
     scatter_tile(k.g, gsl, k.d_table, pt, h, dfeat);
+#endif
   }
 }
 

@@ -14,6 +14,44 @@ import torch
 from . import _lib as L
 
 
+class KernelTimer:
+    """Optional HIP-event timing of the fused launches (bench.py): events are
+    recorded on the same stream the kernels are enqueued on."""
+
+    def __init__(self):
+        self.events = {}
+        self.enabled = False
+
+    def begin(self, name):
+        if not self.enabled:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def end(self, name, start):
+        if start is None:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.events.setdefault(name, []).append((start, e))
+
+    def mean_ms(self, name):
+        ev = self.events.get(name, [])
+        return sum(s.elapsed_time(e) for s, e in ev) / max(len(ev), 1)
+
+    def reset(self):
+        self.events = {}
+
+
+TIMER = KernelTimer()
+
+# Debug hook for parity tests: when True, the fused forward keeps its saved
+# z-values / raw outputs of the last call in LAST (no effect on results).
+DEBUG_KEEP = False
+LAST = {}
+
+
 def _ws(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
@@ -185,7 +223,11 @@ class RenderRaysFn(torch.autograd.Function):
             setattr(a, k, t.data_ptr())
         nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
         wsb = _ws(nbytes, dev)
+        t0 = TIMER.begin("render_fwd")
         L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
+        TIMER.end("render_fwd", t0)
+        if DEBUG_KEEP:
+            LAST.update({k: out[k] for k in ("z_coarse", "z_fine", "raw_c", "raw_f")})
         ctx.cfg = cfg
         ctx.set_materialize_grads(False)   # unused outputs => NULL, not zeros (0*inf)
         ctx.has_noise = (noise_c is not None, noise_f is not None)
@@ -222,7 +264,9 @@ class RenderRaysFn(torch.autograd.Function):
         a.d_fine = L.make_mlp_grad(dws[5:])
         nbytes = L.lib().hn_render_workspace_bytes(ctx.cfg, B)
         wsb = _ws(nbytes, dev)
+        t0 = TIMER.begin("render_bwd")
         L.check(L.lib().hn_render_bwd(ctx.cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_bwd")
+        TIMER.end("render_bwd", t0)
         return (None, None, None, None, None, None, None, d_table, *dws)
 
 

@@ -1,0 +1,145 @@
+"""Training-step driver: the no_batching loop of run_nerf.py:541-651 with
+on-device ray sampling, plus data-parallel gradient exchange.
+
+One step = draw one training image per rank, N_rand pixels without
+replacement (centre crop for the first ``precrop_iters``), render with the
+fused kernels, loss (MSE fine + coarse + sparse_loss_weight * entropy sums
++ tv_loss_weight * TV), backward, gradient all-reduce (DP), RAdam step and
+the exponential lr decay of run_nerf.py:647-651 (applied after step() with
+the pre-increment global_step).
+
+DP semantics: every rank renders its own rays; per-rank MSE
+terms are divided by world_size and the entropy sums are not, so a SUM
+all-reduce yields exactly the gradient of the global-batch reference loss;
+the TV term (one random cube per level) is added on rank 0 only.
+"""
+from __future__ import annotations
+
+import math
+import types
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .create import create_nerf
+from .loss import total_variation_loss
+from .rays import bbox_for_blender, blender_cameras, blender_intrinsics
+from .render import img2mse, mse2psnr, render
+
+
+def default_args(**over):
+    """chair.txt + run_nerf.py defaults (configs/chair.txt:1-19, README.md:20)."""
+    a = dict(N_rand=1024, N_samples=64, N_importance=128, use_viewdirs=True, white_bkgd=True,
+             perturb=1.0, raw_noise_std=0.0, lrate=0.01, lrate_decay=10, precrop_iters=500,
+             precrop_frac=0.5, finest_res=512, log2_hashmap_size=19, sparse_loss_weight=1e-10,
+             tv_loss_weight=1e-6, netchunk=1024 * 64, chunk=1024 * 32, dataset_type="blender",
+             i_embed=1, i_embed_views=2, no_reload=True, ft_path=None, basedir=None, expname=None,
+             H=400, W=400, n_train=100, lindisp=False, no_ndc=False, tv_until=1000)
+    a.update(over)
+    return types.SimpleNamespace(**a)
+
+
+class SyntheticBlender:
+    """Synthetic nerf-synthetic-shaped dataset held in HBM: 100 training
+    cameras on the hemisphere (half-res 400x400, camera_angle_x of chair),
+    bbox from bbox.py's rule, targets uniform in [0,1]^3."""
+
+    def __init__(self, H, W, n, device, seed=0):
+        self.H, self.W = H, W
+        self.focal, self.K = blender_intrinsics(H, W)
+        poses = blender_cameras(n)
+        self.poses = torch.stack(poses, 0).to(device)
+        self.bounding_box = bbox_for_blender(poses, H, W, self.focal)
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.images = torch.rand((n, H, W, 3), generator=g).to(device)
+        self.i_train = torch.arange(n)
+
+
+class Trainer:
+    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0):
+        self.args, self.data, self.device = args, data, torch.device(device)
+        self.rank, self.world = rank, world
+        args.bounding_box = data.bounding_box
+        torch.manual_seed(seed)                      # identical init on every rank
+        (self.kw_train, self.kw_test, self.start, self.grad_vars,
+         self.optimizer) = create_nerf(args, device=self.device)
+        self.embed_fn = self.kw_train["embed_fn"]
+        self.params = list(self.grad_vars) + list(self.embed_fn.parameters())
+        self.global_step = self.start
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(1000003 * seed + 7919 * rank + 1)
+        self.cpu_gen = torch.Generator().manual_seed(seed * 31 + rank)
+        H, W = data.H, data.W
+        jj, ii = torch.meshgrid(torch.arange(H, device=self.device), torch.arange(W, device=self.device),
+                                indexing="ij")
+        self.coords_full = torch.stack([jj, ii], -1).reshape(-1, 2)
+        dH, dW = int(H // 2 * args.precrop_frac), int(W // 2 * args.precrop_frac)
+        cj, ci = torch.meshgrid(torch.arange(H // 2 - dH, H // 2 + dH, device=self.device),
+                                torch.arange(W // 2 - dW, W // 2 + dW, device=self.device), indexing="ij")
+        self.coords_crop = torch.stack([cj, ci], -1).reshape(-1, 2)
+
+    def sample_rays(self, i: int):
+        """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
+        d, a = self.data, self.args
+        img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
+        coords = self.coords_crop if i < a.precrop_iters else self.coords_full
+        sel = torch.randperm(coords.shape[0], device=self.device, generator=self.gen)[: a.N_rand]
+        c = coords[sel]
+        j, ii = c[:, 0].float(), c[:, 1].float()
+        K = d.K
+        dirs = torch.stack([(ii - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -torch.ones_like(ii)], -1)
+        c2w = d.poses[img_i, :3, :4]
+        rays_d = torch.sum(dirs[..., None, :] * c2w[:3, :3], -1)      # ray_util.py:77
+        rays_o = c2w[:3, -1].expand(rays_d.shape)
+        target = d.images[img_i][c[:, 0], c[:, 1]]
+        return torch.stack([rays_o, rays_d], 0), target
+
+    def loss_fn(self, rgb, extras, target, i):
+        a = self.args
+        mse = img2mse(rgb, target)
+        loss = mse
+        if "rgb0" in extras:
+            loss = loss + img2mse(extras["rgb0"], target)
+        loss = loss / self.world
+        sp = extras["sparsity_loss"].sum() + extras["sparsity_loss0"].sum()
+        loss = loss + a.sparse_loss_weight * sp
+        if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
+            e = self.embed_fn
+            tv = sum(total_variation_loss(e.embeddings[l], e.base_resolution, e.finest_resolution, l,
+                                          e.log2_hashmap_size, n_levels=e.n_levels,
+                                          generator=self.cpu_gen) for l in range(e.n_levels))
+            loss = loss + a.tv_loss_weight * tv
+        return loss, mse
+
+    def allreduce_grads(self):
+        if self.world == 1:
+            return
+        table = self.embed_fn.table
+        mlp = [p for p in self.grad_vars if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in mlp])
+        works = [dist.all_reduce(table.grad, async_op=True), dist.all_reduce(flat, async_op=True)]
+        for w in works:
+            w.wait()
+        off = 0
+        for p in mlp:
+            n = p.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p))
+            off += n
+
+    def step(self, i: int):
+        a = self.args
+        batch_rays, target = self.sample_rays(i)
+        rgb, depth, acc, extras = render(self.data.H, self.data.W, self.data.K, chunk=a.chunk,
+                                         rays=batch_rays, retraw=True, near=2., far=6., **self.kw_train)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss, mse = self.loss_fn(rgb, extras, target, i)
+        loss.backward()
+        self.allreduce_grads()
+        self.optimizer.step()
+        decay_steps = a.lrate_decay * 1000
+        new_lr = a.lrate * (0.1 ** (self.global_step / decay_steps))
+        for g in self.optimizer.param_groups:
+            g["lr"] = new_lr
+        self.global_step += 1
+        return loss, mse

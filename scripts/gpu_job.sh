@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU job used with gpurun: tests, smoke, bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+#   usage: scripts/gpu_job.sh [tag] [steps]
+set -o pipefail
+TAG=${1:-r01}
+STEPS=${2:-20}
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+python hashnerf-pytorch_amd/build.py > $OUT/build_$TAG.log 2>&1 || { echo "build failed"; exit 1; }
+timeout -k 10 600 python -m pytest tests -m gpu -q -rf > $OUT/pytest_gpu_$TAG.log 2>&1
+echo "pytest rc=$?" | tee -a $OUT/pytest_gpu_$TAG.log
+tail -4 $OUT/pytest_gpu_$TAG.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 && \
+timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err && \
+cat $OUT/bench_$TAG.json && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o prof -- \
+    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
+echo "chain rc=$?"
+tail -3 $OUT/smoke_$TAG.log
