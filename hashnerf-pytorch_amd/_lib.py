@@ -62,6 +62,22 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
 
 
+class HnTvArgs(C.Structure):
+    _fields_ = [("n_levels", C.c_int32), ("log2_hashmap_size", C.c_int32),
+                ("cube", C.c_int32 * MAX_LEVELS), ("min_vertex", _P), ("table", _P)]
+
+
+RADAM_MAX_TENSORS = 16
+
+
+class HnRadamTensor(C.Structure):
+    _fields_ = [("p", _P), ("g", _P), ("m", _P), ("v", _P), ("n", C.c_int64),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("one_minus_beta1", C.c_float),
+                ("one_minus_beta2", C.c_float), ("eps", C.c_float), ("neg_wd_lr", C.c_float),
+                ("neg_step_lr", C.c_float), ("mode", C.c_int32), ("has_wd", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 # name -> (restype, argtypes); must match include/hashnerf_amd.h exactly.
 SIGNATURES = {
     "hn_abi_version": (C.c_int32, []),
@@ -78,6 +94,9 @@ SIGNATURES = {
     "hn_composite_bwd": (C.c_int32, [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P,
                                      _P, _P, _P, _P]),
     "hn_sample_pdf": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P]),
+    "hn_tv_fwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P]),
+    "hn_tv_bwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P, _P]),
+    "hn_radam_step": (C.c_int32, [C.POINTER(HnRadamTensor), C.c_int32, _P]),
     "hn_render_workspace_bytes": (C.c_size_t, [C.POINTER(HnRenderCfg), C.c_int64]),
     "hn_render_fwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderFwdArgs), _P,
                                   C.c_size_t, _P]),

@@ -1,0 +1,198 @@
+// hn_optim.hip -- the rest of the training step on the device:
+//   * hash-table total variation (loss.py:11-43): all 16 levels' cubes in one
+//     forward launch and one backward launch (the reference issues ~70 eager
+//     ops per level, including a sort-based embedding backward);
+//   * RAdam (radam.py:28-94): every parameter tensor in one launch, dense,
+//     in the reference's per-element op order.
+#include "hn_common.h"
+
+namespace hn {
+
+struct TvK {
+  int32_t L, log2T;
+  int32_t cube[HN_MAX_LEVELS];
+  const int32_t* mv;
+  const float* table;
+};
+
+// Entry of grid vertex (x, y, z) of level l (hash_encoding.py:112-128).
+HN_DEV float2 tv_row(const TvK& k, int l, uint32_t x, uint32_t y, uint32_t z) {
+  const uint32_t mask = (1u << k.log2T) - 1u;
+  const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
+  return ld_row(k.table, (((uint32_t)l << k.log2T) + h) * 8u);
+}
+
+HN_DEV float block_sum_256(float v) {
+  __shared__ float red[4];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void tv_fwd_kernel(TvK k, float* __restrict__ tv) {
+  const int l = blockIdx.y;
+  const int c = k.cube[l], n1 = c + 1;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  float acc = 0.f;
+  if (t < n1 * n1 * n1) {
+    const int i = t / (n1 * n1), j = (t / n1) % n1, kk = t % n1;   // meshgrid 'ij' order
+    const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
+                   z = (uint32_t)(k.mv[3 * l + 2] + kk);
+    const float2 e = tv_row(k, l, x, y, z);
+    if (i < c) { const float2 n = tv_row(k, l, x + 1, y, z); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+    if (j < c) { const float2 n = tv_row(k, l, x, y + 1, z); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+    if (kk < c) { const float2 n = tv_row(k, l, x, y, z + 1); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+  }
+  const float s = block_sum_256(acc);
+  if (threadIdx.x == 0 && s != 0.f) atomic_add_f32(tv + l, s / (float)c);
+}
+
+__global__ __launch_bounds__(256) void tv_bwd_kernel(TvK k, const float* __restrict__ g_tv,
+                                                     float* __restrict__ dtable) {
+  const int l = blockIdx.y;
+  const int c = k.cube[l], n1 = c + 1;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n1 * n1 * n1) return;
+  const int i = t / (n1 * n1), j = (t / n1) % n1, kk = t % n1;
+  const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
+                 z = (uint32_t)(k.mv[3 * l + 2] + kk);
+  const float2 e = tv_row(k, l, x, y, z);
+  float g0 = 0.f, g1 = 0.f;   // sum over incident edges of d(d^2)/de = -+2d
+  const int idx[3] = {i, j, kk};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    if (idx[a] < c) {
+      const float2 n = tv_row(k, l, x + (a == 0), y + (a == 1), z + (a == 2));
+      g0 -= 2.f * (n.x - e.x);
+      g1 -= 2.f * (n.y - e.y);
+    }
+    if (idx[a] > 0) {
+      const float2 pv = tv_row(k, l, x - (a == 0), y - (a == 1), z - (a == 2));
+      g0 += 2.f * (e.x - pv.x);
+      g1 += 2.f * (e.y - pv.y);
+    }
+  }
+  const float scale = g_tv[l] / (float)c;
+  const uint32_t mask = (1u << k.log2T) - 1u;
+  const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
+  float* dst = dtable + ((((size_t)l << k.log2T) + h) << 1);
+  atomic_add_f32(dst, scale * g0);
+  atomic_add_f32(dst + 1, scale * g1);
+}
+
+struct RadamK {
+  int32_t n;
+  hn_radam_tensor t[HN_RADAM_MAX_TENSORS];
+};
+
+// Op forms of torch's CPU kernels (verified bit-exact on the reference's RAdam
+// trace, tests/golden/radam.npz): add_(x, alpha) = fma(alpha, x, self);
+// addcmul_ = fma(value * t1, t2, self); addcdiv_ = self + (value * t1) / t2.
+HN_DEV void radam_elem(const hn_radam_tensor& d, float& p, float g, float& m, float& v) {
+  v = __builtin_fmaf(d.one_minus_beta2 * g, g, v * d.beta2);   // exp_avg_sq.mul_(b2).addcmul_
+  m = __builtin_fmaf(d.one_minus_beta1, g, m * d.beta1);       // exp_avg.mul_(b1).add_
+  if (d.mode != 0) {
+    if (d.has_wd) p = __builtin_fmaf(d.neg_wd_lr, p, p);      // p.add_(-wd*lr, p)
+    if (d.mode == 2) p = p + (d.neg_step_lr * m) / (sqrtf(v) + d.eps);   // addcdiv_
+    else p = __builtin_fmaf(d.neg_step_lr, m, p);              // add_(-step_size*lr, exp_avg)
+  }
+}
+
+__global__ __launch_bounds__(256) void radam_kernel(RadamK k) {
+  const hn_radam_tensor& d = k.t[blockIdx.y];
+  const int64_t n = d.n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool vec = ((n & 3) == 0) && ((((uintptr_t)d.p) | ((uintptr_t)d.g) | ((uintptr_t)d.m) |
+                                       ((uintptr_t)d.v)) & 15) == 0;
+  if (vec) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+      float4 p = reinterpret_cast<float4*>(d.p)[i];
+      const float4 g = reinterpret_cast<const float4*>(d.g)[i];
+      float4 m = reinterpret_cast<float4*>(d.m)[i];
+      float4 v = reinterpret_cast<float4*>(d.v)[i];
+      radam_elem(d, p.x, g.x, m.x, v.x);
+      radam_elem(d, p.y, g.y, m.y, v.y);
+      radam_elem(d, p.z, g.z, m.z, v.z);
+      radam_elem(d, p.w, g.w, m.w, v.w);
+      reinterpret_cast<float4*>(d.m)[i] = m;
+      reinterpret_cast<float4*>(d.v)[i] = v;
+      if (d.mode != 0) reinterpret_cast<float4*>(d.p)[i] = p;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      float p = d.p[i], m = d.m[i], v = d.v[i];
+      radam_elem(d, p, d.g[i], m, v);
+      d.m[i] = m;
+      d.v[i] = v;
+      if (d.mode != 0) d.p[i] = p;
+    }
+  }
+}
+
+static int32_t make_tv(const hn_tv_args* a, TvK& k, int& max_blocks) {
+  if (!a || !a->min_vertex || !a->table) return HN_E_NULL;
+  if (a->n_levels < 1 || a->n_levels > HN_MAX_LEVELS) return HN_E_SHAPE;
+  if (a->log2_hashmap_size < 1 || a->log2_hashmap_size > 24) return HN_E_SHAPE;
+  k.L = a->n_levels;
+  k.log2T = a->log2_hashmap_size;
+  k.mv = a->min_vertex;
+  k.table = a->table;
+  max_blocks = 1;
+  for (int l = 0; l < HN_MAX_LEVELS; ++l) k.cube[l] = l < a->n_levels ? a->cube[l] : 1;
+  for (int l = 0; l < a->n_levels; ++l) {
+    const int c = a->cube[l];
+    if (c < 1 || c > 1000) return HN_E_SHAPE;
+    const int nb = ((c + 1) * (c + 1) * (c + 1) + 255) / 256;
+    max_blocks = nb > max_blocks ? nb : max_blocks;
+  }
+  return HN_OK;
+}
+
+}  // namespace hn
+
+using namespace hn;
+
+extern "C" int32_t hn_tv_fwd(const hn_tv_args* a, float* tv, void* stream) {
+  TvK k;
+  int nb;
+  int32_t st = make_tv(a, k, nb);
+  if (st) return st;
+  if (!tv) return HN_E_NULL;
+  hipStream_t s = (hipStream_t)stream;
+  if ((st = hip_status(hipMemsetAsync(tv, 0, sizeof(float) * a->n_levels, s)))) return st;
+  hipLaunchKernelGGL(tv_fwd_kernel, dim3(nb, a->n_levels), dim3(256), 0, s, k, tv);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_tv_bwd(const hn_tv_args* a, const float* g_tv, float* dtable, void* stream) {
+  TvK k;
+  int nb;
+  int32_t st = make_tv(a, k, nb);
+  if (st) return st;
+  if (!g_tv || !dtable) return HN_E_NULL;
+  hipLaunchKernelGGL(tv_bwd_kernel, dim3(nb, a->n_levels), dim3(256), 0, (hipStream_t)stream, k, g_tv,
+                     dtable);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_radam_step(const hn_radam_tensor* ts, int32_t n_tensors, void* stream) {
+  if (n_tensors < 0 || n_tensors > HN_RADAM_MAX_TENSORS) return HN_E_SHAPE;
+  if (n_tensors == 0) return HN_OK;
+  if (!ts) return HN_E_NULL;
+  RadamK k;
+  k.n = n_tensors;
+  int64_t max_n = 0;
+  for (int i = 0; i < n_tensors; ++i) {
+    if (!ts[i].p || !ts[i].g || !ts[i].m || !ts[i].v) return HN_E_NULL;
+    if (ts[i].n < 0) return HN_E_SHAPE;
+    k.t[i] = ts[i];
+    max_n = ts[i].n > max_n ? ts[i].n : max_n;
+  }
+  int64_t blocks = (max_n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(radam_kernel, dim3((unsigned)blocks, n_tensors), dim3(256), 0, (hipStream_t)stream, k);
+  return hip_status(hipGetLastError());
+}

@@ -270,6 +270,61 @@ class RenderRaysFn(torch.autograd.Function):
         return (None, None, None, None, None, None, None, d_table, *dws)
 
 
+class TVFn(torch.autograd.Function):
+    """Per-level hash-table TV (loss.py:11-43) for all levels in one launch."""
+
+    @staticmethod
+    def forward(ctx, table, min_vertex, cubes, log2T):
+        L.require_device(table)
+        a = L.HnTvArgs()
+        a.n_levels = table.shape[0]
+        a.log2_hashmap_size = int(log2T)
+        for l, c in enumerate(cubes):
+            a.cube[l] = int(c)
+        mv = min_vertex.to(device=table.device, dtype=torch.int32).contiguous()
+        a.min_vertex = mv.data_ptr()
+        a.table = table.data_ptr()
+        tv = torch.empty(table.shape[0], dtype=torch.float32, device=table.device)
+        L.check(L.lib().hn_tv_fwd(a, L.ptr(tv), L.stream(table.device)), "tv_fwd")
+        ctx.save_for_backward(table, mv)
+        ctx.cubes, ctx.log2T = list(cubes), int(log2T)
+        return tv
+
+    @staticmethod
+    def backward(ctx, g_tv):
+        table, mv = ctx.saved_tensors
+        a = L.HnTvArgs()
+        a.n_levels = table.shape[0]
+        a.log2_hashmap_size = ctx.log2T
+        for l, c in enumerate(ctx.cubes):
+            a.cube[l] = int(c)
+        a.min_vertex = mv.data_ptr()
+        a.table = table.data_ptr()
+        dtable = torch.zeros_like(table)
+        g = g_tv.contiguous()
+        L.check(L.lib().hn_tv_bwd(a, L.ptr(g), L.ptr(dtable), L.stream(table.device)), "tv_bwd")
+        return dtable, None, None, None
+
+
+def radam_step(tensors):
+    """tensors: list of (p, g, m, v, coeff dict); one HIP launch per 16 tensors."""
+    for i in range(0, len(tensors), L.RADAM_MAX_TENSORS):
+        chunk = tensors[i:i + L.RADAM_MAX_TENSORS]
+        arr = (L.HnRadamTensor * len(chunk))()
+        dev = chunk[0][0].device
+        for d, (p, g, m, v, c) in zip(arr, chunk):
+            L.require_device(p, g, m, v)
+            for t in (p, g, m, v):
+                if not t.is_contiguous():
+                    raise RuntimeError("hashnerf_amd.radam_step: tensors must be contiguous")
+            d.p, d.g, d.m, d.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+            d.n = p.numel()
+            for k in ("beta1", "beta2", "one_minus_beta1", "one_minus_beta2", "eps", "neg_wd_lr",
+                      "neg_step_lr", "mode", "has_wd"):
+                setattr(d, k, c[k])
+        L.check(L.lib().hn_radam_step(arr, len(chunk), L.stream(dev)), "radam_step")
+
+
 def make_render_cfg(grid: L.HnGrid, white_bkgd: bool, lindisp: bool, perturb: bool,
                     n_samples: int = 64, n_importance: int = 128) -> L.HnRenderCfg:
     c = L.HnRenderCfg()

@@ -6,6 +6,7 @@ from math import exp, floor, log
 
 import torch
 
+from . import functional as HF
 from .embedding import hash as spatial_hash
 
 
@@ -37,6 +38,27 @@ def total_variation_loss(embeddings, min_resolution, max_resolution, level, log2
     tv_y = torch.pow(e[:, 1:] - e[:, :-1], 2).sum()
     tv_z = torch.pow(e[:, :, 1:] - e[:, :, :-1], 2).sum()
     return (tv_x + tv_y + tv_z) / cube.to(dev)
+
+
+def draw_tv_cubes(n_levels, min_resolution, max_resolution, generator=None):
+    """Per-level cube edge and random min vertex, drawn like loss.py:22-25."""
+    cubes, mvs = [], []
+    for l in range(n_levels):
+        resolution, cube = tv_cube(l, n_levels, int(min_resolution), int(max_resolution))
+        cubes.append(int(cube))
+        mvs.append(torch.randint(0, int(resolution - cube), (3,), generator=generator))
+    return cubes, torch.stack(mvs, 0)
+
+
+def tv_loss_levels(embed_fn, generator=None, min_vertex=None):
+    """All 16 ``total_variation_loss`` terms of run_nerf.py:628-635 in one HIP
+    forward (+ one backward) launch.  Returns the per-level values [L]; their
+    sum is the reference's TV_loss."""
+    cubes, mv = draw_tv_cubes(embed_fn.n_levels, embed_fn.base_resolution,
+                              embed_fn.finest_resolution, generator)
+    if min_vertex is not None:
+        mv = min_vertex
+    return HF.TVFn.apply(embed_fn.table, mv, cubes, embed_fn.log2_hashmap_size)
 
 
 def training_loss(rgb, extras, target, sparse_loss_weight=1e-10):

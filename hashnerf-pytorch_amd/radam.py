@@ -3,7 +3,9 @@
 Dense update over every parameter each step (untouched hash rows still get
 their moments decayed), N_sma >= 5 rectification threshold (so no update for
 the first five steps at beta2 = 0.99), weight decay applied as p -= wd*lr*p,
-and the 10-entry step buffer.  Runs as foreach torch ops on the device.
+and the 10-entry step buffer.  The per-element update runs in one HIP launch
+over every parameter (hn_radam_step); the scalar rectification terms are
+computed on the host exactly as the reference does.
 """
 from __future__ import annotations
 
@@ -11,6 +13,8 @@ import math
 
 import torch
 from torch.optim.optimizer import Optimizer
+
+from . import functional as HF
 
 
 class RAdam(Optimizer):
@@ -53,7 +57,9 @@ class RAdam(Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        """All parameters of all groups in one HIP launch (hn_radam_step)."""
         loss = closure() if closure is not None else None
+        work = []
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             for p in group["params"]:
@@ -65,20 +71,17 @@ class RAdam(Optimizer):
                 state = self.state[p]
                 if len(state) == 0:
                     state["step"] = 0
-                    state["exp_avg"] = torch.zeros_like(p)
-                    state["exp_avg_sq"] = torch.zeros_like(p)
-                exp_avg, exp_avg_sq = state["exp_avg"], state["exp_avg_sq"]
-                exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
-                exp_avg.mul_(beta1).add_(grad, alpha=1 - beta1)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 state["step"] += 1
                 n_sma, step_size = self._coeffs(group, state["step"])
-                if n_sma >= 5:
-                    if group["weight_decay"] != 0:
-                        p.add_(p, alpha=-group["weight_decay"] * group["lr"])
-                    denom = exp_avg_sq.sqrt().add_(group["eps"])
-                    p.addcdiv_(exp_avg, denom, value=-step_size * group["lr"])
-                elif step_size > 0:
-                    if group["weight_decay"] != 0:
-                        p.add_(p, alpha=-group["weight_decay"] * group["lr"])
-                    p.add_(exp_avg, alpha=-step_size * group["lr"])
+                mode = 2 if n_sma >= 5 else (1 if step_size > 0 else 0)
+                lr, wd = group["lr"], group["weight_decay"]
+                c = {"beta1": beta1, "beta2": beta2, "one_minus_beta1": 1 - beta1,
+                     "one_minus_beta2": 1 - beta2, "eps": group["eps"], "neg_wd_lr": -wd * lr,
+                     "neg_step_lr": -step_size * lr if mode else 0.0, "mode": mode,
+                     "has_wd": int(wd != 0)}
+                work.append((p, grad.contiguous(), state["exp_avg"], state["exp_avg_sq"], c))
+        if work:
+            HF.radam_step(work)
         return loss

@@ -23,7 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .create import create_nerf
-from .loss import total_variation_loss
+from .loss import tv_loss_levels
 from .rays import bbox_for_blender, blender_cameras, blender_intrinsics
 from .render import img2mse, mse2psnr, render
 
@@ -105,10 +105,7 @@ class Trainer:
         sp = extras["sparsity_loss"].sum() + extras["sparsity_loss0"].sum()
         loss = loss + a.sparse_loss_weight * sp
         if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
-            e = self.embed_fn
-            tv = sum(total_variation_loss(e.embeddings[l], e.base_resolution, e.finest_resolution, l,
-                                          e.log2_hashmap_size, n_levels=e.n_levels,
-                                          generator=self.cpu_gen) for l in range(e.n_levels))
+            tv = tv_loss_levels(self.embed_fn, generator=self.cpu_gen).sum()
             loss = loss + a.tv_loss_weight * tv
         return loss, mse
 

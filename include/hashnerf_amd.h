@@ -167,6 +167,41 @@ typedef struct hn_render_bwd_args {
   hn_mlp_grad d_coarse; hn_mlp_grad d_fine;
 } hn_render_bwd_args;
 
+/* ---- L4 hash-table total variation (loss.py:11-43), all levels at once ---
+ * Level l samples the cube of (cube[l]+1)^3 grid vertices starting at
+ * min_vertex[l] (device int32 [L][3], the reference's torch.randint draw),
+ * hashes them like hash_encoding.py:112-128 and sums squared differences of
+ * the entries along x, y and z, divided by cube[l]. */
+typedef struct hn_tv_args {
+  int32_t n_levels;
+  int32_t log2_hashmap_size;
+  int32_t cube[HN_MAX_LEVELS];
+  const int32_t* min_vertex;   /* device [L][3] */
+  const float* table;          /* device [L][2^T][2] */
+} hn_tv_args;
+/* tv[L] (device) is overwritten with the per-level TV values. */
+int32_t hn_tv_fwd(const hn_tv_args* a, float* tv, void* stream);
+/* dtable += sum_l g_tv[l] * d tv_l / d table  (g_tv: device [L]). */
+int32_t hn_tv_bwd(const hn_tv_args* a, const float* g_tv, float* dtable, void* stream);
+
+/* ---- L4 RAdam step (radam.py:28-94) over many tensors in one launch -----
+ * Per element, in the op forms of torch's CPU kernels (bit-exact on the
+ * reference's trace):
+ *   v = fma((1-beta2)*g, g, v*beta2) ; m = fma(1-beta1, g, m*beta1)
+ *   mode 2 (N_sma >= 5): p = fma(neg_wd_lr, p, p) (if wd); p += (neg_step_lr*m)/(sqrt(v)+eps)
+ *   mode 1 (step_size > 0, N_sma < 5): p = fma(neg_wd_lr, p, p) (if wd); p = fma(neg_step_lr, m, p)
+ *   mode 0: moments only (the reference's first steps at beta2=0.99).
+ * Scalars are the fp32 values torch would use (host computes N_sma/step_size). */
+#define HN_RADAM_MAX_TENSORS 16
+typedef struct hn_radam_tensor {
+  float* p; const float* g; float* m; float* v; int64_t n;
+  float beta1, beta2, one_minus_beta1, one_minus_beta2, eps, neg_wd_lr, neg_step_lr;
+  int32_t mode;
+  int32_t has_wd;
+  int32_t reserved;
+} hn_radam_tensor;
+int32_t hn_radam_step(const hn_radam_tensor* ts, int32_t n_tensors, void* stream);
+
 size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
 int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
                       void* workspace, size_t ws_bytes, void* stream);

@@ -251,3 +251,39 @@ def test_fused_matches_unfused_large(hn):
     close(a_t, b_t.cpu().numpy(), rtol=1e-2, atol=1e-3 * scale, msg="table grad")
     for x, y in zip(a_w, b_w):
         close(x, y.cpu().numpy(), rtol=1e-2, atol=1e-3 * y.abs().max().item(), msg="mlp grad")
+
+
+@pytest.mark.parametrize("finest", [512, 1024])
+def test_tv_all_levels_vs_reference(hn, finest):
+    """hn_tv_fwd/bwd (one launch each) against loss.py:11-43 per level."""
+    from importlib import import_module
+    HF = import_module("hashnerf_pytorch_amd.functional")
+    HL = import_module("hashnerf_pytorch_amd.loss")
+    g = golden(f"tv_f{finest}")
+    tab = g2t(pcg_table(g["table_seed"], g["log2T"])).requires_grad_(True)
+    cubes, _ = HL.draw_tv_cubes(16, 16, finest)
+    tv = HF.TVFn.apply(tab, torch.from_numpy(g["min_vertex"]), cubes, int(g["log2T"]))
+    close(tv, g["tv"], rtol=2e-5, atol=1e-7, msg="tv")
+    tv.sum().backward()
+    for l in range(16):
+        close(tab.grad[l], g["grad"][l], rtol=1e-5, atol=1e-7, msg=f"tv grad level {l}")
+
+
+def test_radam_trace_vs_reference(hn):
+    """hn_radam_step (one launch, two param groups) against the reference's
+    8-step RAdam trace: no update for steps 1-5 (N_sma < 5), then adaptive."""
+    g = golden("radam")
+    pa = torch.nn.Parameter(g2t(g["p0"]).clone())
+    pb = torch.nn.Parameter(g2t(g["t0"]).clone())
+    opt = hn.RAdam([{"params": [pa], "weight_decay": 1e-6}, {"params": [pb], "eps": 1e-15}],
+                   lr=0.01, betas=(0.9, 0.99))
+    for step in range(8):
+        pa.grad = g2t(g["ga"][step]).clone()
+        pb.grad = g2t(g["gb"][step]).clone()
+        opt.step()
+        for gr in opt.param_groups:
+            gr["lr"] = 0.01 * (0.1 ** ((step + 1) / 500000))
+        # bit-exact: same op forms as torch's CPU kernels (fma placement)
+        np.testing.assert_array_equal(pa.detach().cpu().numpy(), g["pa"][step], f"pa step {step}")
+        np.testing.assert_array_equal(pb.detach().cpu().numpy(), g["pb"][step], f"pb step {step}")
+    assert opt.state[pa]["step"] == 8
