@@ -51,13 +51,14 @@ class HnRenderFwdArgs(C.Structure):
                 ("noise_c", _P), ("noise_f", _P), ("table", _P), ("coarse", HnMlp), ("fine", HnMlp),
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
-                ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P)]
+                ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
+                ("fine_src", _P)]
 
 
 class HnRenderBwdArgs(C.Structure):
     _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("noise_c", _P), ("noise_f", _P), ("table", _P),
                 ("coarse", HnMlp), ("fine", HnMlp), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P),
-                ("raw_f", _P), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
+                ("raw_f", _P), ("fine_src", _P), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
 

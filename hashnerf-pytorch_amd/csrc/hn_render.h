@@ -320,8 +320,11 @@ HN_DEV void sample_pdf_wave(const float* bins, const float* w, int nw, float* cd
 }
 
 // Sort S (<= 256) floats of src (LDS) into dst (LDS) by rank; ties keep
-// source order.  Values are what torch.sort returns (indices are unused).
-HN_DEV void rank_sort_wave(const float* src, float* dst, int S, int lane) {
+// source order.  Values are what torch.sort returns.  If origin != null,
+// origin[rank] = e for source elements e < n_tag, else 255 (where each sorted
+// element came from: lets the backward merge a coarse sample's two passes).
+HN_DEV void rank_sort_wave(const float* src, float* dst, int S, int lane, uint8_t* origin = nullptr,
+                           int n_tag = 0) {
   for (int e = lane; e < S; e += 64) {
     const float v = src[e];
     int rank = 0;
@@ -330,6 +333,7 @@ HN_DEV void rank_sort_wave(const float* src, float* dst, int S, int lane) {
       rank += (o < v || (o == v && j < e)) ? 1 : 0;
     }
     dst[rank] = v;
+    if (origin != nullptr) origin[rank] = e < n_tag ? (uint8_t)e : (uint8_t)255;
   }
   lds_fence_wave();
 }

@@ -44,6 +44,7 @@ struct RenderK {
   const float* Pf;
   float *rgb, *depth, *acc, *sparsity, *rgb0, *depth0, *acc0, *sparsity0, *z_std;
   float *z_coarse, *z_fine, *raw_c, *raw_f;
+  uint8_t* fine_src;
 };
 
 struct RenderBK {
@@ -57,10 +58,12 @@ struct RenderBK {
   const float* Pc;
   const float* Pf;
   const float *z_coarse, *z_fine, *raw_c, *raw_f;
+  const uint8_t* fine_src;
   const float *g_rgb, *g_depth, *g_acc, *g_sparsity, *g_rgb0, *g_depth0, *g_acc0, *g_sparsity0;
   const float* g_raw_f;
   float* d_table;
   float* slab;    // [kBwdBlocks][W_END]
+  float* dfeat;   // [B][64 + 192][32]: d loss / d feature per evaluated point
 };
 
 struct Ray {
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(RenderK k) {
     const double var = wave_sum(d0 * d0 + d1 * d1) / kNi;
     if (lane == 0) k.z_std[ray] = (float)sqrt(var);
   }
-  rank_sort_wave(zsrc, zs, kSf, lane);
+  rank_sort_wave(zsrc, zs, kSf, lane, k.fine_src + ray * kSf, kSc);
   for (int i = lane; i < kSf; i += 64) k.z_fine[ray * kSf + i] = zs[i];
 
   // ---- fine network (:556) ----
@@ -372,10 +375,131 @@ HN_DEV void bwd_ray(const RenderBK& k, int64_t ray, bool fine, float* Wacc, floa
     const float rgbg[3] = {dr.x, dr.y, dr.z};
     mlp_bwd_tile(P, feat, shx8, a, dy2, dr.w, rgbg, T, Wacc, dfeat, nullptr, lane);
 #endif
+    // per-point feature gradient stored [point][feature f][level] for the
+    // scatter kernel (lane half h holds levels tile_level(m, h))
+    float* dst = k.dfeat + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + q) * 32;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int l = h ? tile_level(m, 1) : tile_level(m, 0);
+      dst[l] = dfeat[2 * m];
+      dst[16 + l] = dfeat[2 * m + 1];
+    }
+  }
+}
+
+// Scatter of the table gradient, one wave per ray over its 192 UNIQUE points:
+// a fine sample that is one of the 64 coarse samples (fine_src < 64) is the
+// same point in both passes, so its coarse-pass and fine-pass feature grads
+// are summed before the trilinear backward + atomics (25 % fewer atomics).
+// Few registers -> high occupancy to keep many atomics in flight; kept out of
+// the MFMA kernel so the atomics never stall its gathers on vmcnt.
+//
+// Lane layout: 16 points per pass, 4 lanes per point = (x offset i, feature f).
+// One atomic wave-instruction then covers corners (0,j,k) and (1,j,k) of both
+// features of 16 points: h(x+1) differs from h(x) only in low bits (prime 1
+// on x), so 7/8 of the x-pairs fall in one 64-byte segment and the four dwords
+// of a point go out as ~1 memory request instead of 2 (the float-atomic path
+// is request-rate bound for random rows).  Consecutive points are consecutive
+// samples along the ray; runs inside one voxel are summed first (segmented
+// suffix sum over points) and only the run head issues atomics.
+HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
+                            const float pt[3], const float xc[3], uint32_t l, float gl, int pp,
+                            int xi, int f) {
+  const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
+  uint32_t cell[3];
+  float w[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float q = (xc[a] - g.bmin[a]) / gs[a];
+    const int32_t i = (int32_t)floorf(q);
+    const float vmin = (float)i * gs[a] + g.bmin[a];
+    const float vmax = vmin + gs[a];
+    w[a] = (pt[a] - vmin) / (vmax - vmin);
+    cell[a] = (uint32_t)i;
+  }
+  const uint32_t mask = (1u << g.log2T) - 1u;
+  const uint32_t hx = cell[0] + (uint32_t)xi;
+  const uint32_t y0 = cell[1] * kPrimeY, y1 = (cell[1] + 1u) * kPrimeY;
+  const uint32_t z0 = cell[2] * kPrimeZ, z1 = (cell[2] + 1u) * kPrimeZ;
+  // d feat / d e_c = ((g * fz) * fy) * fx  (trilerp_bwd order), c = 4*xi + jk
+  const float fx = xi ? w[0] : 1.f - w[0];
+  const float gz0 = gl * (1.f - w[2]), gz1 = gl * w[2];
+  float cv[4];
+  cv[0] = (gz0 * (1.f - w[1])) * fx;   // j=0 k=0
+  cv[1] = (gz1 * (1.f - w[1])) * fx;   // j=0 k=1
+  cv[2] = (gz0 * w[1]) * fx;           // j=1 k=0
+  cv[3] = (gz1 * w[1]) * fx;           // j=1 k=1
+  const uint32_t q0 = __shfl_up(cell[0], 4, 64), q1 = __shfl_up(cell[1], 4, 64),
+                 q2 = __shfl_up(cell[2], 4, 64);
+  const bool head = pp == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
+  const uint64_t hm = __ballot(head);
+  uint32_t pm = 0;                                  // one head bit per point
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pm |= (uint32_t)((hm >> (4 * j)) & 1u) << j;
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
+    if (!__any(same)) break;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float o = __shfl_down(cv[c], 4 * d, 64);
+      if (same) cv[c] += o;
+    }
+  }
+  if (head) {
+    const uint32_t row0 = l << g.log2T;
+    const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
+                            (hx ^ y1 ^ z1) & mask};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
+                                            (row0 + hh[c]) * 8u + 4u * f);
+      atomic_add_f32(dst, cv[c]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void render_scatter_kernel(RenderBK k) {
+  __shared__ float gsl[kGsLds];
+  stage_grid_sizes(k.g, gsl);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int pp = lane >> 2, xi = (lane >> 1) & 1, f = lane & 1;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= k.B) return;
+  Ray r;
+  load_ray(k.rays, ray, r);
+  const float* base = k.dfeat + (size_t)ray * (kSc + kSf) * 32;
+  for (int grp = 0; grp < kSf / 16; ++grp) {
+    const int q = 16 * grp + pp;
+    float pt[3], xc[3];
+    ray_point(r, k.z_fine[ray * kSf + q], pt);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
+    const int src = k.fine_src[ray * kSf + q];
+    float gl[16];
+    const float* df = base + (size_t)(kSc + q) * 32 + 16 * f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 v = *reinterpret_cast<const float4*>(df + 4 * t);
+      gl[4 * t] = v.x; gl[4 * t + 1] = v.y; gl[4 * t + 2] = v.z; gl[4 * t + 3] = v.w;
+    }
+    if (src < kSc) {
+      const float* dc = base + (size_t)src * 32 + 16 * f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 v = *reinterpret_cast<const float4*>(dc + 4 * t);
+        gl[4 * t] += v.x; gl[4 * t + 1] += v.y; gl[4 * t + 2] += v.z; gl[4 * t + 3] += v.w;
+      }
+    }
 #if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
-    if (dfeat[0] == 1234.5f && dfeat[1] == -1234.5f) k.d_table[lane] = dfeat[2];
+    if (gl[0] == 1234.5f && gl[1] == -1234.5f) k.d_table[lane] = gl[2];
 #else
-    scatter_tile(k.g, gsl, k.d_table, pt, h, dfeat);
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+      scatter_level_x(k.g, gsl, k.d_table, pt, xc, l, gl[l], pp, xi, f);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #endif
   }
 }
@@ -440,10 +564,12 @@ static bool grad_ok(const hn_mlp_grad& w) {
 
 using namespace hn;
 
+// Workspace: packed coarse + fine weights | dW slabs [256][9344] |
+// per-point feature grads [n_rays][256][32].
 extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays) {
   (void)cfg;
-  (void)n_rays;
-  return ((size_t)2 * G_END + (size_t)kBwdBlocks * W_END) * sizeof(float);
+  const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
+  return ((size_t)2 * G_END + (size_t)kBwdBlocks * W_END + n * (kSc + kSf) * 32) * sizeof(float);
 }
 
 extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
@@ -457,7 +583,8 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
     return HN_E_NULL;
   if (cfg->perturb && !a->t_rand) return HN_E_NULL;
   if (!a->rgb || !a->depth || !a->acc || !a->sparsity || !a->rgb0 || !a->depth0 || !a->acc0 ||
-      !a->sparsity0 || !a->z_std || !a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f)
+      !a->sparsity0 || !a->z_std || !a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f ||
+      !a->fine_src)
     return HN_E_NULL;
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
@@ -478,7 +605,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.rgb = a->rgb; k.depth = a->depth; k.acc = a->acc; k.sparsity = a->sparsity;
   k.rgb0 = a->rgb0; k.depth0 = a->depth0; k.acc0 = a->acc0; k.sparsity0 = a->sparsity0;
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
-  k.raw_c = a->raw_c; k.raw_f = a->raw_f;
+  k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdWaves - 1) / kFwdWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdWaves), 0, s, k);
   return hip_status(hipGetLastError());
@@ -492,7 +619,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (a->n_rays < 0) return HN_E_SHAPE;
   if (a->n_rays == 0) return HN_OK;
   if (!a->rays || !a->table || !mlp_ok(a->coarse) || !mlp_ok(a->fine)) return HN_E_NULL;
-  if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f) return HN_E_NULL;
+  if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f || !a->fine_src) return HN_E_NULL;
   if (!a->d_table || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
@@ -500,6 +627,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
+  float* dfeat = slab + (size_t)kBwdBlocks * W_END;
   if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
   if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
   RenderBK k;
@@ -509,6 +637,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.rays = a->rays; k.noise_c = a->noise_c; k.noise_f = a->noise_f; k.table = a->table;
   k.Pc = Pc; k.Pf = Pf;
   k.z_coarse = a->z_coarse; k.z_fine = a->z_fine; k.raw_c = a->raw_c; k.raw_f = a->raw_f;
+  k.fine_src = a->fine_src;
+  k.dfeat = dfeat;
   k.g_rgb = a->g_rgb; k.g_depth = a->g_depth; k.g_acc = a->g_acc; k.g_sparsity = a->g_sparsity;
   k.g_rgb0 = a->g_rgb0; k.g_depth0 = a->g_depth0; k.g_acc0 = a->g_acc0;
   k.g_sparsity0 = a->g_sparsity0; k.g_raw_f = a->g_raw_f;
@@ -516,6 +646,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.slab = slab;
   const size_t lds = (size_t)(W_END + kBwdWaves * kBLds + kGsLds) * sizeof(float);
   hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kBwdWaves), lds, s, k);
+  if ((st = hip_status(hipGetLastError()))) return st;
+  hipLaunchKernelGGL(render_scatter_kernel, dim3((unsigned)((a->n_rays + 3) / 4)), dim3(256), 0, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 255) / 256), dim3(256), 0, s, slab,
                      a->d_coarse, a->d_fine);

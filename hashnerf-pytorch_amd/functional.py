@@ -221,6 +221,8 @@ class RenderRaysFn(torch.autograd.Function):
         a.fine = L.make_mlp(ws[5:])
         for k, t in out.items():
             setattr(a, k, t.data_ptr())
+        fine_src = torch.empty((B, 192), dtype=torch.uint8, device=dev)
+        a.fine_src = fine_src.data_ptr()
         nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
         wsb = _ws(nbytes, dev)
         t0 = TIMER.begin("render_fwd")
@@ -233,14 +235,14 @@ class RenderRaysFn(torch.autograd.Function):
         ctx.has_noise = (noise_c is not None, noise_f is not None)
         ctx.save_for_backward(rays, noise_c if noise_c is not None else rays,
                               noise_f if noise_f is not None else rays, table, out["z_coarse"],
-                              out["z_fine"], out["raw_c"], out["raw_f"], *ws)
+                              out["z_fine"], out["raw_c"], out["raw_f"], fine_src, *ws)
         ctx.mark_non_differentiable(out["z_std"])
         return (out["rgb"], out["depth"], out["acc"], out["sparsity"], out["rgb0"], out["depth0"],
                 out["acc0"], out["sparsity0"], out["z_std"], out["raw_f"])
 
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_acc, g_sp, g_rgb0, g_depth0, g_acc0, g_sp0, _g_zstd, g_raw):
-        rays, noise_c, noise_f, table, z_c, z_f, raw_c, raw_f, *ws = ctx.saved_tensors
+        rays, noise_c, noise_f, table, z_c, z_f, raw_c, raw_f, fine_src, *ws = ctx.saved_tensors
         noise_c = noise_c if ctx.has_noise[0] else None
         noise_f = noise_f if ctx.has_noise[1] else None
         B = rays.shape[0]
@@ -260,6 +262,7 @@ class RenderRaysFn(torch.autograd.Function):
             t = L.contig(t)
             keep.append(t)
             setattr(a, k, None if t is None else t.data_ptr())
+        a.fine_src = fine_src.data_ptr()
         a.d_coarse = L.make_mlp_grad(dws[:5])
         a.d_fine = L.make_mlp_grad(dws[5:])
         nbytes = L.lib().hn_render_workspace_bytes(ctx.cfg, B)

@@ -149,6 +149,7 @@ typedef struct hn_render_fwd_args {
   float* z_fine;            /* [B][192] */
   float* raw_c;             /* [B][64][4] */
   float* raw_f;             /* [B][192][4] */
+  uint8_t* fine_src;        /* [B][192]: coarse index of each fine sample, 255 = importance */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -158,6 +159,7 @@ typedef struct hn_render_bwd_args {
   const float* table;
   hn_mlp coarse; hn_mlp fine;
   const float* z_coarse; const float* z_fine; const float* raw_c; const float* raw_f;
+  const uint8_t* fine_src;  /* from the forward */
   /* upstream grads (NULL = 0) */
   const float* g_rgb; const float* g_depth; const float* g_acc; const float* g_sparsity;
   const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;

@@ -15,7 +15,7 @@ tail -4 $OUT/pytest_gpu_$TAG.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 && \
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err && \
 cat $OUT/bench_$TAG.json && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o prof -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o prof -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
 echo "chain rc=$?"
 tail -3 $OUT/smoke_$TAG.log
