@@ -105,19 +105,28 @@ def main():
     ap.add_argument("--n-rand", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    cfg_id = args.config or (2 if world == 1 else 4)
+    # same per-GPU workload at every N (weak scaling); --config 4 selects the
+    # 8192-rays-per-GPU DP configuration of BASELINE configs[3]
+    cfg_id = args.config or 2
     cfg = dict(CONFIGS[cfg_id])
     if args.n_rand:
         cfg["N_rand"] = args.n_rand
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; modulo only matters for single-GPU gloo rehearsals
+    local_dev = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     import hn_loader
     hn = hn_loader.load()

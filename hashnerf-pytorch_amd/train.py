@@ -28,6 +28,39 @@ from .rays import bbox_for_blender, blender_cameras, blender_intrinsics
 from .render import img2mse, mse2psnr, render
 
 
+def dp_loss(mse_fine, mse_coarse, entropy_sum, world, sparse_loss_weight, tv=None,
+            tv_loss_weight=0.0):
+    """Per-rank loss whose SUM-all-reduced gradient equals the gradient of the
+    reference loss (run_nerf.py:612-636) over the global batch: the MSE terms
+    are means (divide by world), the entropy term is a sum over rays (do not),
+    and the TV term is counted once (pass tv on one rank only)."""
+    loss = (mse_fine + (mse_coarse if mse_coarse is not None else 0.0)) / world
+    loss = loss + sparse_loss_weight * entropy_sum
+    if tv is not None:
+        loss = loss + tv_loss_weight * tv
+    return loss
+
+
+def allreduce_grads(table, mlp_params, group=None):
+    """SUM all-reduce of the hash-table gradient (one big bucket, 64 MiB at
+    T=19) and of the flattened NeRFSmall gradients (one small bucket), issued
+    asynchronously back to back so RCCL can run them concurrently."""
+    mlp = [p for p in mlp_params if p.grad is not None]
+    flat = torch.cat([p.grad.reshape(-1) for p in mlp]) if mlp else None
+    works = []
+    if table.grad is not None:
+        works.append(dist.all_reduce(table.grad, group=group, async_op=True))
+    if flat is not None:
+        works.append(dist.all_reduce(flat, group=group, async_op=True))
+    for w in works:
+        w.wait()
+    off = 0
+    for p in mlp:
+        n = p.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p))
+        off += n
+
+
 def default_args(**over):
     """chair.txt + run_nerf.py defaults (configs/chair.txt:1-19, README.md:20)."""
     a = dict(N_rand=1024, N_samples=64, N_importance=128, use_viewdirs=True, white_bkgd=True,
@@ -98,31 +131,17 @@ class Trainer:
     def loss_fn(self, rgb, extras, target, i):
         a = self.args
         mse = img2mse(rgb, target)
-        loss = mse
-        if "rgb0" in extras:
-            loss = loss + img2mse(extras["rgb0"], target)
-        loss = loss / self.world
+        mse0 = img2mse(extras["rgb0"], target) if "rgb0" in extras else None
         sp = extras["sparsity_loss"].sum() + extras["sparsity_loss0"].sum()
-        loss = loss + a.sparse_loss_weight * sp
+        tv = None
         if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
             tv = tv_loss_levels(self.embed_fn, generator=self.cpu_gen).sum()
-            loss = loss + a.tv_loss_weight * tv
+        loss = dp_loss(mse, mse0, sp, self.world, a.sparse_loss_weight, tv, a.tv_loss_weight)
         return loss, mse
 
     def allreduce_grads(self):
-        if self.world == 1:
-            return
-        table = self.embed_fn.table
-        mlp = [p for p in self.grad_vars if p.grad is not None]
-        flat = torch.cat([p.grad.reshape(-1) for p in mlp])
-        works = [dist.all_reduce(table.grad, async_op=True), dist.all_reduce(flat, async_op=True)]
-        for w in works:
-            w.wait()
-        off = 0
-        for p in mlp:
-            n = p.numel()
-            p.grad.copy_(flat[off:off + n].view_as(p))
-            off += n
+        if self.world > 1:
+            allreduce_grads(self.embed_fn.table, self.grad_vars)
 
     def step(self, i: int):
         a = self.args

@@ -1,0 +1,39 @@
+#!/bin/bash
+# PMC counter passes (one counter group per rocprofv3 run, --kernel-trace only,
+# as MI355X_MICROARCH.md prescribes) over a short bench; per-kernel averages
+# per dispatch go to gpurun_out/pmc_<tag>.txt.
+#   usage: scripts/gpu_pmc.sh TAG [bench args...]
+set -o pipefail
+TAG=${1:-m}
+shift
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+python hashnerf-pytorch_amd/build.py > $OUT/build_$TAG.log 2>&1 || { echo "build failed"; exit 1; }
+rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+PASSES=("FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum"
+        "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_F32"
+        "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS")
+i=0
+for P in "${PASSES[@]}"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $OUT/pmc_${TAG}_$i -o pmc -- \
+      python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline "$@" > $OUT/pmc_${TAG}_$i.log 2>&1 \
+      || echo "pass $i ($P) failed: $(tail -2 $OUT/pmc_${TAG}_$i.log)"
+done
+python3 - "$OUT" "$TAG" <<'EOF' | tee $OUT/pmc_$2.txt
+import csv, glob, sys, collections
+out, tag = sys.argv[1], sys.argv[2]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in sorted(glob.glob(f"{out}/pmc_{tag}_*/**/*counter_collection.csv", recursive=True)):
+    for r in csv.DictReader(open(f)):
+        name = r.get("Kernel_Name", r.get("Kernel-Name", ""))
+        if not name.startswith("hn::"):
+            continue
+        key = name.split("(")[0]
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in sorted(agg.items()):
+    print(k)
+    for c, v in sorted(cs.items()):
+        print(f"   {c:32s} avg/dispatch {sum(v)/len(v):.6g}  (n={len(v)})")
+EOF

@@ -1,0 +1,137 @@
+"""Data-parallel semantics on CPU with world_size=2 over gloo.
+
+(1) allreduce_grads sums the hash-table gradient and the flattened MLP
+    gradients across ranks.
+(2) The per-rank loss rule (train.dp_loss: MSE / world, entropy sums not
+    scaled, TV on one rank) makes the SUM-all-reduced gradient equal to the
+    reference loss gradient over the global batch (run_nerf.py:612-636).
+    Checked with the CPU oracle as the renderer (test infrastructure only).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene(B=24, T=12):
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import hashnerf_oracle as O
+    g = torch.Generator().manual_seed(7)
+    box = (torch.tensor([-4.0, -4.0, -3.4]), torch.tensor([4.0, 4.0, 3.3]))
+    tab = (torch.rand(16, 2 ** T, 2, generator=g) * 2 - 1) * 0.5
+    wc = O.init_nerf_small(g)
+    wf = O.init_nerf_small(g)
+    c2w = O.pose_spherical(20.0, -30.0, 4.0)
+    focal = 0.5 * 100 / np.tan(0.5 * 0.6911112070083618)
+    K = np.array([[focal, 0, 50.0], [0, focal, 50.0], [0, 0, 1]])
+    ro, rd = O.get_rays(100, 100, K, c2w[:3, :4])
+    sel = torch.randperm(100 * 100, generator=g)[:B]
+    ro, rd = ro.reshape(-1, 3)[sel], rd.reshape(-1, 3)[sel]
+    vd = rd / torch.norm(rd, dim=-1, keepdim=True)
+    rb = torch.cat([ro, rd, 2 * torch.ones(B, 1), 6 * torch.ones(B, 1), vd], -1)
+    t_rand = torch.rand(B, 64, generator=g)
+    u = torch.rand(B, 128, generator=g)
+    target = torch.rand(B, 3, generator=g)
+    mv = torch.stack([torch.randint(0, 5, (3,), generator=g) for _ in range(16)])
+    return O, box, tab, wc, wf, rb, t_rand, u, target, mv, T
+
+
+def _grads(O, box, tab, wc, wf, rb, t_rand, u, target, mv, T, loss_fn):
+    tab = tab.clone().requires_grad_(True)
+    wc = {k: v.clone().requires_grad_(True) for k, v in wc.items()}
+    wf = {k: v.clone().requires_grad_(True) for k, v in wf.items()}
+    ret = O.render_rays(rb, wc, wf, tab, box[0], box[1], O.level_resolutions(16, 16, 512), T,
+                        t_rand=t_rand, u=u, white_bkgd=True)
+    tv = sum(O.total_variation_loss(tab[l], l, mv[l], T) for l in range(16))
+    loss = loss_fn(ret, target, tv)
+    loss.backward()
+    return tab, [wc[k] for k in O.MLP_KEYS] + [wf[k] for k in O.MLP_KEYS]
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import allreduce_grads, dp_loss
+    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene()
+    B = rb.shape[0]
+    sl = slice(rank * B // world, (rank + 1) * B // world)
+
+    def loss_fn(ret, tgt, tv):
+        mse = torch.mean((ret["rgb_map"] - tgt) ** 2)
+        mse0 = torch.mean((ret["rgb0"] - tgt) ** 2)
+        ent = ret["sparsity_loss"].sum() + ret["sparsity_loss0"].sum()
+        return dp_loss(mse, mse0, ent, world, 1e-3, tv if rank == 0 else None, 1e-2)
+
+    tab_g, mlp = _grads(O, box, tab, wc, wf, rb[sl], t_rand[sl], u[sl], target[sl], mv, T, loss_fn)
+    allreduce_grads(tab_g, mlp)
+    if rank == 0:
+        torch.save({"table": tab_g.grad, "mlp": [p.grad for p in mlp]}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_grads_sums(tmp_path):
+    port = _free_port()
+    mp.spawn(_allreduce_worker, args=(2, port, str(tmp_path / "ar.pt")), nprocs=2, join=True)
+    got = torch.load(tmp_path / "ar.pt", weights_only=True)
+    assert torch.equal(got["table"], torch.full((3, 8, 2), 3.0))
+    assert torch.equal(got["mlp"][0], torch.full((4, 5), 30.0))
+    assert torch.equal(got["mlp"][1], torch.full((7,), 300.0))
+
+
+def _allreduce_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import allreduce_grads
+    table = torch.nn.Parameter(torch.zeros(3, 8, 2))
+    table.grad = torch.full((3, 8, 2), float(rank + 1))
+    ps = [torch.nn.Parameter(torch.zeros(4, 5)), torch.nn.Parameter(torch.zeros(7))]
+    ps[0].grad = torch.full((4, 5), 10.0 * (rank + 1))
+    ps[1].grad = torch.full((7,), 100.0 * (rank + 1))
+    allreduce_grads(table, ps)
+    if rank == 0:
+        torch.save({"table": table.grad, "mlp": [p.grad for p in ps]}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_gradient_equals_global_batch(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path / "dp.pt")), nprocs=2, join=True)
+    got = torch.load(tmp_path / "dp.pt", weights_only=True)
+    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene()
+
+    def ref_loss(ret, tgt, tv):   # run_nerf.py:612-636 on the whole batch
+        return (torch.mean((ret["rgb_map"] - tgt) ** 2) + torch.mean((ret["rgb0"] - tgt) ** 2)
+                + 1e-3 * (ret["sparsity_loss"].sum() + ret["sparsity_loss0"].sum()) + 1e-2 * tv)
+
+    tab_g, mlp = _grads(O, box, tab, wc, wf, rb, t_rand, u, target, mv, T, ref_loss)
+    ref = tab_g.grad
+    err = (got["table"] - ref).norm() / ref.norm()
+    assert err < 1e-5, err
+    for a, p in zip(got["mlp"], mlp):
+        e = (a - p.grad).norm() / p.grad.norm()
+        assert e < 1e-5, e
