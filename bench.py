@@ -41,6 +41,23 @@ UNIQUE_PTS = 192               # per ray (the 64 coarse points recur in the fine
 PATH_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2 + 36
 BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2        # bwd kernel: re-gather + scatter-add
 FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
+BWD_KERNELS = ("render_bwd_kernel", "render_scatter_kernel", "slab_reduce_kernel")
+
+
+def measured_traffic(cfg_id, n_rand_override):
+    """HBM-side bytes per hn_render_bwd launch from the last PMC passes of the
+    same workload (scripts/gpu_pmc.sh -> profiles/traffic_config<N>.json):
+    2 x FETCH_SIZE + WRITE_SIZE summed over the launch's kernels.  PMC
+    counters need their own rocprofv3 passes, so bench.py cannot collect
+    them live; None when no file matches this workload."""
+    path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}.json")
+    if n_rand_override or not os.path.exists(path):
+        return None, None
+    t = json.load(open(path))
+    ks = t.get("kernels", {})
+    if not all(k in ks for k in BWD_KERNELS):
+        return None, None
+    return sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in BWD_KERNELS), t.get("source")
 
 
 def cpu_baseline(cfg, seconds=12.0, n_rays=256):
@@ -165,6 +182,7 @@ def main():
     B = cfg["N_rand"]
     value = world * B * args.steps / dt
     if rank == 0:
+        traffic, traffic_src = measured_traffic(cfg_id, args.n_rand)
         bwd_gbs = B * BWD_BYTES_PER_RAY / (bwd_ms * 1e-3) / 1e9
         fwd_gbs = B * FWD_BYTES_PER_RAY / (fwd_ms * 1e-3) / 1e9
         line = {
@@ -178,7 +196,10 @@ def main():
                        "finest_res": cfg["finest_res"], "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "kernel": "render_bwd (hn_render_bwd launch)",
                          "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(bwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": round(traffic) if traffic else None,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": B * BWD_BYTES_PER_RAY,
                          "bytes_per_ray": BWD_BYTES_PER_RAY, "launch_ms": round(bwd_ms, 4)},
             "kernels": {"render_fwd_ms": round(fwd_ms, 4), "render_fwd_GBs": round(fwd_gbs, 1),
                         "render_bwd_ms": round(bwd_ms, 4),

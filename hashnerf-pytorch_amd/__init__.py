@@ -9,7 +9,7 @@ RAdam, total_variation_loss); the arithmetic runs in the HIP C-ABI library
 from . import _lib
 from .create import create_nerf
 from .embedding import HashEmbedder, SHEncoder, hash, level_resolutions
-from .loss import total_variation_loss, training_loss
+from .loss import sigma_sparsity_loss, total_variation_loss, training_loss
 from .models import NeRFSmall
 from .radam import RAdam
 from .rays import get_ndc_rays, get_rays, get_rays_np, pose_spherical
@@ -18,5 +18,5 @@ from .render import (NetworkQuery, batchify, img2mse, mse2psnr, raw2outputs, ren
 
 __all__ = ["HashEmbedder", "SHEncoder", "NeRFSmall", "RAdam", "create_nerf", "render", "render_rays",
            "render_path", "raw2outputs", "sample_pdf", "run_network", "batchify", "NetworkQuery",
-           "total_variation_loss", "training_loss", "get_rays", "get_rays_np", "get_ndc_rays",
+           "total_variation_loss", "sigma_sparsity_loss", "training_loss", "get_rays", "get_rays_np", "get_ndc_rays",
            "pose_spherical", "img2mse", "mse2psnr", "hash", "level_resolutions"]

@@ -10,6 +10,13 @@ from . import functional as HF
 from .embedding import hash as spatial_hash
 
 
+def sigma_sparsity_loss(sigmas):
+    """loss.py:45-47 (Cauchy sparsity on sigma).  Imported by run_nerf.py:19
+    but unused on the training path (run_nerf_helpers.py:608 is commented
+    out); kept for import compatibility as plain torch ops."""
+    return torch.log(1.0 + 2 * sigmas ** 2).sum(dim=-1)
+
+
 def tv_cube(level, n_levels, min_resolution, max_resolution):
     """Resolution and cube edge of loss.py:13-22 (float64 math, floor, clip)."""
     b = exp((log(max_resolution) - log(min_resolution)) / (n_levels - 1))
