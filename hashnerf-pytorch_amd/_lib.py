@@ -16,6 +16,8 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
+ABI_VERSION = 2                 # HN_ABI_VERSION
+RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 24064
 
@@ -52,13 +54,13 @@ class HnRenderFwdArgs(C.Structure):
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
                 ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
-                ("fine_src", _P)]
+                ("fine_src", _P), ("feat", _P)]
 
 
 class HnRenderBwdArgs(C.Structure):
     _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("noise_c", _P), ("noise_f", _P), ("table", _P),
                 ("coarse", HnMlp), ("fine", HnMlp), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P),
-                ("raw_f", _P), ("fine_src", _P), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
+                ("raw_f", _P), ("fine_src", _P), ("feat", _P), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
 

@@ -8,6 +8,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic ablations (never set in the product build; scripts/ablate.sh):
+// 1 = no scatter atomics, 2 = no MLP in the render backward, 3 = no weight
+// gradients (transposes staged, no MFMA / accumulation), 4 = weight-gradient
+// MFMAs without the LDS accumulation.
+#ifndef HN_ABLATE
+#define HN_ABLATE 0
+#endif
+
 #include "../../include/hashnerf_amd.h"
 
 #define HN_DEV __device__ __forceinline__
@@ -200,12 +208,31 @@ HN_DEV void sh16(float x, float y, float z, float o[16]) {
 // ---------------------------------------------------------------------------
 // Wave (64-lane) primitives
 // ---------------------------------------------------------------------------
-HN_DEV int lane_id() { return (int)__lane_id(); }
+// The lane index behind an empty asm: the optimiser cannot treat it as loop-
+// invariant, so persistent kernels do not hoist every shuffle's address and
+// lane-compare mask out of their work loop (hundreds of registers).
+HN_DEV int lane_id() {
+  int l = (int)__lane_id();
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
+// v from lane src (ds_bpermute; exact move).
+HN_DEV float shfl_from(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+HN_DEV double shfl_from(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
 template <typename T>
 HN_DEV T wave_sum(T v) {
+  const int l = lane_id();
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o >= 1; o >>= 1) v += shfl_from(v, l ^ o);
   return v;
 }
 
@@ -214,7 +241,7 @@ HN_DEV double wave_incl_sum(double v) {
   const int l = lane_id();
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const double t = __shfl_up(v, o, 64);
+    const double t = shfl_from(v, l >= o ? l - o : l);
     if (l >= o) v += t;
   }
   return v;
@@ -223,7 +250,7 @@ HN_DEV double wave_incl_prod(double v) {
   const int l = lane_id();
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const double t = __shfl_up(v, o, 64);
+    const double t = shfl_from(v, l >= o ? l - o : l);
     if (l >= o) v *= t;
   }
   return v;

@@ -48,8 +48,9 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 // the scheduling barrier stops hipcc from hoisting all loads (register blowup).
 template <int KS, typename BF>
 HN_DEV f32x16 gemm(const float* __restrict__ P, int off, int ob, f32x16 acc, int lane, BF bval) {
-  // opaque: keep hipcc from hoisting ~50 uniform GEMM base addresses into SGPRs
-  const float* base = opaque_ptr(P + off + ob * (KS / 4) * 256) + lane * 4;
+  // opaque BEFORE the offset: keeps hipcc from precomputing ~50 uniform GEMM
+  // base addresses at the top of the tile loop (SGPR pairs that then spill)
+  const float* base = opaque_ptr(P) + off + ob * (KS / 4) * 256 + lane * 4;
   f32x4 an = *reinterpret_cast<const f32x4*>(base);
 #pragma unroll
   for (int g = 0; g < KS / 4; ++g) {
@@ -150,10 +151,17 @@ HN_DEV void accum_block(float* acc_lds, int base, int ld, int n0, int nmax, int 
 // One staged weight-gradient block: Tdy/Tx already hold the operands.
 HN_DEV void wgrad_accum(const float* Tdy, const float* Tx, float* Wacc, int base, int ld, int n0,
                         int nmax, int k0, int kmax, int lane) {
+#if HN_ABLATE == 3
+  return;
+#endif
   lds_fence_wave();
   const f32x16 d = wgrad_block(Tdy, Tx, lane);
   lds_fence_wave();
+#if HN_ABLATE == 4
+  if (d[0] == 1234.5f && d[1] == -1234.5f) Wacc[lane] = d[2];
+#else
   accum_block(Wacc, base, ld, n0, nmax, k0, kmax, d, lane);
+#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 

@@ -24,7 +24,7 @@ HN_DEV void excl_prod(const double (&x)[N], double (&T)[N], int lane) {
 #pragma unroll
   for (int k = 0; k < N; ++k) loc *= x[k];
   const double inc = wave_incl_prod(loc);
-  double ex = __shfl_up(inc, 1, 64);
+  double ex = shfl_from(inc, lane > 0 ? lane - 1 : 0);
   if (lane == 0) ex = 1.0;
 #pragma unroll
   for (int k = 0; k < N; ++k) { T[k] = ex; ex *= x[k]; }
@@ -37,7 +37,7 @@ HN_DEV void excl_suffix_sum(const double (&v)[N], double (&S)[N], int lane) {
 #pragma unroll
   for (int k = 0; k < N; ++k) loc += v[k];
   const double inc = wave_incl_sum(loc);          // prefix incl. this lane
-  const double tot = __shfl(inc, 63, 64);
+  const double tot = shfl_from(inc, 63);
   double after = tot - inc;                       // sum of later lanes
 #pragma unroll
   for (int k = N - 1; k >= 0; --k) { S[k] = after; after += v[k]; }

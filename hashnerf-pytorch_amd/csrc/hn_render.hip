@@ -9,25 +9,19 @@
 //   6 fine tiles (encode + MLP) -> composite (:558).
 // Backward, one wave64 per ray, workgroups specialised per network (coarse
 // blocks / fine blocks, so each keeps ONE network's dW accumulator in LDS):
-//   composite backward (wave suffix scan) -> per tile: re-encode, recompute the
-//   MLP, MLP backward on MFMA (dW through LDS transposes, accumulated in LDS),
-//   trilinear backward + float atomics into the hash-table gradient.
+//   composite backward (wave suffix scan) -> per tile: load the features the
+//   forward saved, recompute the MLP, MLP backward on MFMA (dW through LDS
+//   transposes, accumulated in LDS), store d loss / d feature per point.
+// Scatter kernel, one wave per ray over its 192 unique points: trilinear
+// backward + float atomics into the hash-table gradient.
 #include "hn_mlp.h"
 #include "hn_render.h"
-
-// Diagnostic ablations (never set in the product build): 1 = no scatter
-// atomics, 2 = no MLP in the backward (gather + scatter only).
-#ifndef HN_ABLATE
-#define HN_ABLATE 0
-#endif
 
 namespace hn {
 
 constexpr int kSc = 64, kNi = 128, kSf = 192;
 constexpr int kFwdWaves = 4;
-constexpr int kBwdWaves = 8;
-constexpr int kBwdBlocks = 256;          // persistent: one 512-thread block per CU
-constexpr int kBwdCoarseBlocks = 64;     // coarse work is 2 tiles/ray, fine 6
+constexpr int kBwdBlocks = 256;          // persistent backward: one block per CU
 
 struct RenderK {
   GridArgs g;
@@ -45,6 +39,7 @@ struct RenderK {
   float *rgb, *depth, *acc, *sparsity, *rgb0, *depth0, *acc0, *sparsity0, *z_std;
   float *z_coarse, *z_fine, *raw_c, *raw_f;
   uint8_t* fine_src;
+  float* feat;    // [B][8 tiles][1024] saved features or NULL
 };
 
 struct RenderBK {
@@ -59,11 +54,27 @@ struct RenderBK {
   const float* Pf;
   const float *z_coarse, *z_fine, *raw_c, *raw_f;
   const uint8_t* fine_src;
+  const float* feat;   // [B][8 tiles][1024] features saved by the forward
   const float *g_rgb, *g_depth, *g_acc, *g_sparsity, *g_rgb0, *g_depth0, *g_acc0, *g_sparsity0;
   const float* g_raw_f;
   float* d_table;
-  float* slab;    // [kBwdBlocks][W_END]
+  float* slab;    // [kBwdBlocks][2][W_END]: per-block dW (coarse | fine)
   float* dfeat;   // [B][64 + 192][32]: d loss / d feature per evaluated point
+};
+
+// Arguments of the backward MLP kernel (kept lean: every field lives in SGPRs).
+struct B1K {
+  int64_t B;
+  int white;
+  const float* rays;
+  const float *noise_c, *noise_f;
+  const float *Pc, *Pf;
+  const float *z_coarse, *z_fine, *raw_c, *raw_f;
+  const float* feat;
+  const float *g_rgb, *g_depth, *g_acc, *g_sparsity, *g_rgb0, *g_depth0, *g_acc0, *g_sparsity0;
+  const float* g_raw_f;
+  float* slab;
+  float* dfeat;
 };
 
 struct Ray {
@@ -89,6 +100,30 @@ HN_DEV void ray_point(const Ray& r, float z, float pt[3]) {
   for (int a = 0; a < 3; ++a) pt[a] = r.o[a] + r.d[a] * z;
 }
 
+// Saved features: tile t of a ray (t = 0,1 coarse, 2..7 fine) is 1024 floats,
+// stored as 4 chunks of [64 lanes][float4] so that both the forward's store
+// and the backward's load are fully coalesced dwordx4 accesses.
+constexpr int kTilesPerRay = (kSc + kSf) / 32;
+static_assert(kTilesPerRay * 1024 == HN_RENDER_FEAT_PER_RAY, "feature cache layout");
+
+HN_DEV void store_feat(float* __restrict__ base, int64_t ray, int tile, int lane, const f32x16& feat) {
+  f32x4* t = reinterpret_cast<f32x4*>(base + ((size_t)ray * kTilesPerRay + tile) * 1024);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 v = {feat[4 * c], feat[4 * c + 1], feat[4 * c + 2], feat[4 * c + 3]};
+    __builtin_nontemporal_store(v, t + 64 * c + lane);
+  }
+}
+
+HN_DEV void load_feat(const float* __restrict__ base, int64_t ray, int tile, int lane, f32x16& feat) {
+  const f32x4* t = reinterpret_cast<const f32x4*>(base + ((size_t)ray * kTilesPerRay + tile) * 1024);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 v = __builtin_nontemporal_load(t + 64 * c + lane);
+    feat[4 * c] = v.x; feat[4 * c + 1] = v.y; feat[4 * c + 2] = v.z; feat[4 * c + 3] = v.w;
+  }
+}
+
 // Hash-encode one point into the 32-feature tile layout (lane half h owns
 // levels tile_level(m, h), m = 0..7).  hash_encoding.py:84-110.
 HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __restrict__ table, const float pt[3], int h,
@@ -109,72 +144,6 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     feat[2 * m] = f0;
     feat[2 * m + 1] = f1;
     if (m & 1) __builtin_amdgcn_sched_barrier(0);   // <= 16 gathers in flight
-  }
-}
-
-// One level of the scatter for the 32 points of a tile (lane half h adds
-// feature h; both halves see the same point and level, so the f0/f1 atomics
-// of an entry are two adjacent dwords of ONE wave-instruction = one memory
-// request).  Consecutive lanes are consecutive samples along the ray; a run
-// of samples inside one voxel shares all 8 corners, so the run is summed in
-// registers first (segmented suffix sum over the half-wave) and only its head
-// lane issues the 8 atomics.  The reduction is skipped when the level has no
-// run (fine levels, sparse samples).
-HN_DEV void scatter_level(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
-                          const float pt[3], const float xc[3], uint32_t l, float gf, int p, int h) {
-  const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
-  const uint32_t mask = (1u << g.log2T) - 1u;
-  Voxel v;
-  uint32_t cell[3];
-  voxel_level_cell(pt, xc, gs, g.bmin, mask, v, cell);
-  float cv[8];
-  trilerp_bwd(gf, v.w, cv);
-  const uint32_t q0 = __shfl_up(cell[0], 1, 32), q1 = __shfl_up(cell[1], 1, 32),
-                 q2 = __shfl_up(cell[2], 1, 32);
-  const bool head = p == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
-  const uint32_t hm = (uint32_t)(__ballot(head) >> (32 * h));   // heads of this half
-#pragma unroll
-  for (int d = 1; d < 32; d <<= 1) {
-    // lane p absorbs lane p+d iff no run starts in (p, p+d]
-    const bool same = p + d < 32 && ((hm >> (p + 1)) & ((1u << d) - 1u)) == 0u;
-    if (!__any(same)) break;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float o = __shfl_down(cv[c], d, 32);
-      if (same) cv[c] += o;
-    }
-  }
-  if (head) {
-    const uint32_t row0 = l << g.log2T;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
-                                            (row0 + v.h[c]) * 8u + 4u * h);
-      atomic_add_f32(dst, cv[c]);
-    }
-  }
-}
-
-// Trilinear backward + scatter-add of one tile's feature grads into the table
-// gradient (embedding_dense_backward of hash_encoding.py:106).
-HN_DEV void scatter_tile(const GridArgs& g, const float* gsl, float* __restrict__ dtable, const float pt[3], int h,
-                         const f32x16& dfeat) {
-  const int p = lane_id() & 31;
-  float xc[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], g.bmin[a], g.bmax[a]);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    // lane half h holds (f0, f1) of level tile_level(m, h); trade so that
-    // half h holds feature h of both levels tile_level(m, 0/1)
-    const float g0 = dfeat[2 * m], g1 = dfeat[2 * m + 1];
-    const float recv = __shfl_xor(h ? g0 : g1, 32, 64);
-    const float ga = h ? recv : g0;     // feature h of level tile_level(m, 0)
-    const float gb = h ? g1 : recv;     // feature h of level tile_level(m, 1)
-    scatter_level(g, gsl, dtable, pt, xc, tile_level(m, 0), ga, p, h);
-    __builtin_amdgcn_sched_barrier(0);
-    scatter_level(g, gsl, dtable, pt, xc, tile_level(m, 1), gb, p, h);
-    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -248,6 +217,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(RenderK k) {
     ray_point(r, zc[q], pt);
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
+    if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
@@ -292,6 +262,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(RenderK k) {
     ray_point(r, zs[q], pt);
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
+    if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
@@ -314,25 +285,196 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(RenderK k) {
   }
 }
 
-// LDS per backward wave (floats) after the workgroup's dW accumulator.
-constexpr int kBT = 0, kBZ = 2 * kTBuf, kBRaw = kBZ + kSf, kBLds = kBRaw + 4 * kSf;
-static_assert((W_END + kBRaw) % 4 == 0, "float4 alignment of the raw buffer");
+// ---------------------------------------------------------------------------
+// Backward MLP kernel (B1).  One wave per SIMD (4 per CU, 512 registers each):
+// the wave keeps ALL twelve 32x32 weight-gradient blocks of its network as
+// MFMA accumulators (192 registers, AGPR-resident) for the whole kernel, so a
+// tile's dW costs only its MFMAs -- no per-tile LDS accumulation.  The
+// operands of the dW products (the point index on the MFMA k axis) come from
+// per-wave [row][point] LDS images (row stride kXS = 36 floats: staging
+// ds_write_b32 and the ds_read_b128 operand reads are bank-conflict-free);
+// k-step s of lane half h contracts point 16h + s, so four k-steps are one
+// ds_read_b128 per operand.  ReLU masks are kept as bits.
+//
+// Work units: a coarse unit is one ray's 2 coarse tiles, a fine unit 2 of a
+// ray's 6 fine tiles (each fine unit redoes the ray's cheap composite
+// backward).  Wave 0 of every block runs coarse units, waves 1-3 fine units:
+// 1 : 3 matches the 2 : 6 tile ratio, so every wave gets the same tile count.
+// ---------------------------------------------------------------------------
+constexpr int kXS = 36;
+// image rows per wave: features | h0 | [sh16 | geo15] | c0 | c1 | rgb grads
+constexpr int kRF = 0, kRH0 = 32, kRC0in = 96, kRC0 = 128, kRC1 = 192, kRC2 = 256, kRRows = 260;
+constexpr int kB1Waves = 4;
+constexpr int kB1Lds = kB1Waves * kRRows * kXS;            // floats (149,760 B)
+static_assert(kB1Lds >= 2 * W_END, "final dW reduction reuses the images");
+static_assert(kRRows * kXS % 4 == 0 && kXS % 4 == 0, "b128 alignment");
 
-template <int S>
-HN_DEV void bwd_ray(const RenderBK& k, int64_t ray, bool fine, float* Wacc, float* L, const float* gsl,
-                    int lane) {
-  constexpr int N = S / 64;
+struct DW {
+  f32x16 c2[2], c1[4], c0[2], s1[2], s0[2];
+};
+
+// image rows [row0, row0 + 32) <- D-layout tile (row row_of(r,h), point p)
+HN_DEV void put_rows(float* X, int row0, const f32x16& v, int lane) {
   const int p = lane & 31, h = lane >> 5;
-  float* T = L + kBT;
-  float* zb = L + kBZ;
-  float* rawb = L + kBRaw;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) X[(row0 + row_of(r, h)) * kXS + p] = v[r];
+}
+
+// acc[n][k] += sum over the tile's 32 points of A[arow_n][pt] * B[brow_k][pt];
+// arow / brow are this lane's rows (n = k = lane & 31).
+HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
+  const int h = lane >> 5;
+  const f32x4* pa = reinterpret_cast<const f32x4*>(X + arow * kXS + 16 * h);
+  const f32x4* pb = reinterpret_cast<const f32x4*>(X + brow * kXS + 16 * h);
+  f32x4 an = pa[0], bn = pb[0];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 a = an, b = bn;
+    if (g < 3) {
+      an = pa[g + 1];
+      bn = pb[g + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma(a[j], b[j], acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return acc;
+}
+
+HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    m |= (v[r] > 0.f ? 1u : 0u) << (16 * ob + r);
+    v[r] = v[r] > 0.f ? v[r] : 0.f;
+  }
+}
+HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) g[r] = (m >> (16 * ob + r)) & 1u ? g[r] : 0.f;
+}
+
+// One 32-point tile: recompute the forward (features from the cache), then
+// the MLP backward; dW into the wave's accumulators, d feature to dst.
+HN_DEV void b1_tile(const float* __restrict__ P, float* X, const f32x16& feat, const f32x16 c0sh[2],
+                    float4 dr, DW& dw, float* __restrict__ dst) {
+  const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
+  const int p = lane & 31, h = lane >> 5, i = lane & 31;
+  uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
+  // ---- forward recompute (models.py:151-174) ----
+  put_rows(X, kRF, feat, lane);
+  f32x16 h0[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    h0[ob] = gemm<16>(P, G_F0, ob, zero16(), lane, [&](int s) { return feat[s]; });
+    relu_bits(h0[ob], mh0, ob);
+    put_rows(X, kRH0 + 32 * ob, h0[ob], lane);
+  }
+  const f32x16 s1 = gemm<32>(P, G_F1, 0, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {                 // geo rows 1..15 -> image rows 16..30
+    const int row = row_of(r, h);
+    if (row >= 1) X[(kRC0in + 15 + row) * kXS + p] = s1[r];
+  }
+  f32x16 c0[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    c0[ob] = gemm<8>(P, G_F2G, ob, c0sh[ob], lane, [&](int s) { return s1[s]; });
+    relu_bits(c0[ob], mc0, ob);
+    put_rows(X, kRC0 + 32 * ob, c0[ob], lane);
+  }
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    f32x16 c1 = gemm<32>(P, G_F3, ob, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    relu_bits(c1, mc1, ob);
+    put_rows(X, kRC1 + 32 * ob, c1, lane);
+  }
+  if (h == 0) {
+    X[(kRC2 + 0) * kXS + p] = dr.x;
+    X[(kRC2 + 1) * kXS + p] = dr.y;
+    X[(kRC2 + 2) * kXS + p] = dr.z;
+  }
+  lds_fence_wave();
+  // ---- color_net.2 ----
+  const int rc2 = kRC2 + (i < 3 ? i : 3);       // rows >= 3 of this block are discarded
+  dw.c2[0] = wgrad(X, rc2, kRC1 + i, dw.c2[0], lane);
+  dw.c2[1] = wgrad(X, rc2, kRC1 + 32 + i, dw.c2[1], lane);
+  const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
+  f32x16 dc1[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    dc1[ob] = gemm<4>(P, G_B4, ob, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+    mask_bits(dc1[ob], mc1, ob);
+  }
+  lds_fence_wave();
+  // ---- color_net.1 (dc1 image over the c1 rows) ----
+  put_rows(X, kRC1, dc1[0], lane);
+  put_rows(X, kRC1 + 32, dc1[1], lane);
+  lds_fence_wave();
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      dw.c1[2 * nb + kb] = wgrad(X, kRC1 + 32 * nb + i, kRC0 + 32 * kb + i, dw.c1[2 * nb + kb], lane);
+  f32x16 dc0[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    dc0[ob] = gemm<32>(P, G_B3, ob, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+    mask_bits(dc0[ob], mc0, ob);
+  }
+  lds_fence_wave();
+  // ---- color_net.0: X = [sh16 | geo15] (dc0 image over the c0 rows) ----
+  put_rows(X, kRC0, dc0[0], lane);
+  put_rows(X, kRC0 + 32, dc0[1], lane);
+  lds_fence_wave();
+  dw.c0[0] = wgrad(X, kRC0 + i, kRC0in + i, dw.c0[0], lane);
+  dw.c0[1] = wgrad(X, kRC0 + 32 + i, kRC0in + i, dw.c0[1], lane);
+  f32x16 ds1 = gemm<32>(P, G_B2G, 0, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+  if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
+  // ---- sigma_net.1 (ds1 image over the c1 rows; rows 16..31 are zero) ----
+  put_rows(X, kRC1, ds1, lane);
+  lds_fence_wave();
+  dw.s1[0] = wgrad(X, kRC1 + i, kRH0 + i, dw.s1[0], lane);
+  dw.s1[1] = wgrad(X, kRC1 + i, kRH0 + 32 + i, dw.s1[1], lane);
+  f32x16 dh0[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    dh0[ob] = gemm<8>(P, G_B1, ob, zero16(), lane, [&](int s) { return ds1[s]; });
+    mask_bits(dh0[ob], mh0, ob);
+  }
+  // ---- sigma_net.0 (dh0 image over the c0 rows) ----
+  put_rows(X, kRC0, dh0[0], lane);
+  put_rows(X, kRC0 + 32, dh0[1], lane);
+  lds_fence_wave();
+  dw.s0[0] = wgrad(X, kRC0 + i, kRF + i, dw.s0[0], lane);
+  dw.s0[1] = wgrad(X, kRC0 + 32 + i, kRF + i, dw.s0[1], lane);
+  const f32x16 dfeat = gemm<32>(P, G_B0, 0, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  // per-point feature gradient stored [point][feature f][level] for the
+  // scatter kernel (lane half h holds levels tile_level(m, h))
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int l = h ? tile_level(m, 1) : tile_level(m, 0);
+    dst[l] = dfeat[2 * m];
+    dst[16 + l] = dfeat[2 * m + 1];
+  }
+  lds_fence_wave();                             // image reads done before the next tile's writes
+}
+
+// One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
+template <int S>
+HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw) {
+  const int lane = lane_id();
+  constexpr int N = S / 64;
+  constexpr bool fine = S == kSf;
+  const int p = lane & 31, h = lane >> 5;
+  float* zb = X + kRC0 * kXS;                   // scratch over the c0 / c1 rows
+  float* rawb = zb + S;
   Ray r;
   load_ray(k.rays, ray, r);
   const float* zsrc = (fine ? k.z_fine : k.z_coarse) + ray * S;
   const float* rsrc = (fine ? k.raw_f : k.raw_c) + ray * S * 4;
-  for (int i = lane; i < S; i += 64) {
-    zb[i] = zsrc[i];
-    *reinterpret_cast<float4*>(rawb + 4 * i) = *reinterpret_cast<const float4*>(rsrc + 4 * i);
+  for (int j = lane; j < S; j += 64) {
+    zb[j] = zsrc[j];
+    *reinterpret_cast<float4*>(rawb + 4 * j) = *reinterpret_cast<const float4*>(rsrc + 4 * j);
   }
   lds_fence_wave();
   CompGrad g;
@@ -354,37 +496,78 @@ HN_DEV void bwd_ray(const RenderBK& k, int64_t ray, bool fine, float* Wacc, floa
   const float* graw = (fine && k.g_raw_f) ? k.g_raw_f + ray * S * 4 : nullptr;
   composite_bwd<N>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
   lds_fence_wave();
+  const int tile0 = 2 * part;                   // tile within this pass
+  float4 dr[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(rawb + 4 * (32 * (tile0 + t) + p));
   float sh8[8], shx8[8];
   ray_sh(r, h, sh8, shx8);
-  for (int tau = 0; tau < S / 32; ++tau) {
-    const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
-    const int q = 32 * tau + p;
-    float pt[3];
-    ray_point(r, zb[q], pt);
-    f32x16 feat;
-    encode_tile(k.g, gsl, k.table, pt, h, feat);
-    f32x16 dfeat;
-#if HN_ABLATE == 2   // diagnostic build: gather + scatter only (no MLP)
-    dfeat = feat;
-#else
-    MlpAct a;
-    f32x16 c2;
-    mlp_fwd_tile(P, feat, sh8, a, c2, lane);
-    const float4 dr = *reinterpret_cast<const float4*>(rawb + 4 * q);
-    const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
-    const float rgbg[3] = {dr.x, dr.y, dr.z};
-    mlp_bwd_tile(P, feat, shx8, a, dy2, dr.w, rgbg, T, Wacc, dfeat, nullptr, lane);
-#endif
-    // per-point feature gradient stored [point][feature f][level] for the
-    // scatter kernel (lane half h holds levels tile_level(m, h))
-    float* dst = k.dfeat + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + q) * 32;
+  lds_fence_wave();
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int l = h ? tile_level(m, 1) : tile_level(m, 0);
-      dst[l] = dfeat[2 * m];
-      dst[16 + l] = dfeat[2 * m + 1];
-    }
+  for (int j = 0; j < 8; ++j) X[(kRC0in + 8 * h + j) * kXS + p] = shx8[j];
+  const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
+  // color_net.0 applied to the sh part: the same for every point of the ray
+  // (and bit-identical to starting each point's chain with it)
+  f32x16 c0sh[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob)
+    c0sh[ob] = gemm<8>(P, G_F2S, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+  const int ctile = (fine ? kSc / 32 : 0) + tile0;
+  f32x16 feat, featn;
+  load_feat(k.feat, ray, ctile, lane, feat);
+  load_feat(k.feat, ray, ctile + 1, lane, featn);
+  float* dbase = k.dfeat + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0)) * 32;
+  b1_tile(P, X, feat, c0sh, dr[0], dw, dbase + (size_t)(32 * tile0 + p) * 32);
+  b1_tile(P, X, featn, c0sh, dr[1], dw, dbase + (size_t)(32 * (tile0 + 1) + p) * 32);
+}
+
+// acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS).
+HN_DEV void dw_flush(float* acc, int base, int ld, int n0, int nmax, int k0, int kmax, const f32x16& d,
+                     int lane) {
+  accum_block(acc, base, ld, n0, nmax, k0, kmax, d, lane);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void render_bwd_kernel(B1K k) {
+  extern __shared__ f32x4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  float* X = smem + wave * kRRows * kXS;
+  const bool fine = wave != 0;
+  DW dw;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) dw.c2[j] = dw.c0[j] = dw.s1[j] = dw.s0[j] = zero16();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
+  if (!fine) {
+    for (int64_t ray = blockIdx.x; ray < k.B; ray += gridDim.x) b1_unit<kSc>(k, ray, 0, X, dw);
+  } else {
+    const int64_t n_units = 3 * k.B;
+    for (int64_t u = (int64_t)blockIdx.x * 3 + (wave - 1); u < n_units; u += (int64_t)gridDim.x * 3)
+      b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw);
   }
+  // block reduction of the waves' dW (coarse | fine) into LDS, then one slab
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * W_END; j += blockDim.x) smem[j] = 0.f;
+  __syncthreads();
+  float* acc = smem + (fine ? W_END : 0);
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) dw_flush(acc, W_C2, 64, 0, 3, 32 * kb, 64, dw.c2[kb], lane);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      dw_flush(acc, W_C1, 64, 32 * nb, 64, 32 * kb, 64, dw.c1[2 * nb + kb], lane);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) dw_flush(acc, W_C0, 31, 32 * nb, 64, 0, 31, dw.c0[nb], lane);
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) dw_flush(acc, W_S1, 64, 0, 16, 32 * kb, 64, dw.s1[kb], lane);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) dw_flush(acc, W_S0, 32, 32 * nb, 64, 0, 32, dw.s0[nb], lane);
+  __syncthreads();
+  float* slab = k.slab + (size_t)blockIdx.x * 2 * W_END;
+  for (int j = threadIdx.x; j < 2 * W_END; j += blockDim.x) slab[j] = smem[j];
 }
 
 // Scatter of the table gradient, one wave per ray over its 192 UNIQUE points:
@@ -504,38 +687,22 @@ __global__ __launch_bounds__(256) void render_scatter_kernel(RenderBK k) {
   }
 }
 
-__global__ __launch_bounds__(512, 2) void render_bwd_kernel(RenderBK k) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Wacc = smem;
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  float* L = smem + W_END + wave * kBLds;
-  float* gsl = smem + W_END + kBwdWaves * kBLds;
-  stage_grid_sizes(k.g, gsl);
-  for (int i = threadIdx.x; i < W_END; i += blockDim.x) Wacc[i] = 0.f;
-  __syncthreads();
-  const bool fine = blockIdx.x >= kBwdCoarseBlocks;
-  const int blk = fine ? blockIdx.x - kBwdCoarseBlocks : blockIdx.x;
-  const int nblk = fine ? kBwdBlocks - kBwdCoarseBlocks : kBwdCoarseBlocks;
-  for (int64_t ray = (int64_t)blk * kBwdWaves + wave; ray < k.B; ray += (int64_t)nblk * kBwdWaves) {
-    if (fine) bwd_ray<kSf>(k, ray, true, Wacc, L, gsl, lane);
-    else bwd_ray<kSc>(k, ray, false, Wacc, L, gsl, lane);
-  }
-  __syncthreads();
-  float* dst = k.slab + (size_t)blockIdx.x * W_END;
-  for (int i = threadIdx.x; i < W_END; i += blockDim.x) dst[i] = Wacc[i];
-}
-
-// dW(coarse) += sum of coarse-block slabs, dW(fine) += sum of fine-block slabs.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab,
+// dW(coarse) += sum_b slab[b][0], dW(fine) += sum_b slab[b][1].  64
+// consecutive elements per block, 4 block-groups per element, LDS combine.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs,
                                                           hn_mlp_grad dc, hn_mlp_grad df) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * W_END) return;
-  const bool fine = t >= W_END;
-  const int i = fine ? t - W_END : t;
-  const int b0 = fine ? kBwdCoarseBlocks : 0, b1 = fine ? kBwdBlocks : kBwdCoarseBlocks;
+  __shared__ float part[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
   float s = 0.f;
-  for (int b = b0; b < b1; ++b) s += slab[(size_t)b * W_END + i];
+  if (e < 2 * W_END)
+    for (int b = grp; b < n_slabs; b += 4) s += slab[(size_t)b * 2 * W_END + e];
+  part[grp][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (grp != 0 || e >= 2 * W_END) return;
+  s = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+  const bool fine = e >= W_END;
+  const int i = fine ? e - W_END : e;
   const hn_mlp_grad& d = fine ? df : dc;
   float* dst;
   if (i < W_S1) dst = d.sigma0 + i;
@@ -564,12 +731,12 @@ static bool grad_ok(const hn_mlp_grad& w) {
 
 using namespace hn;
 
-// Workspace: packed coarse + fine weights | dW slabs [256][9344] |
+// Workspace: packed coarse + fine weights | dW slabs [256][2][9344] |
 // per-point feature grads [n_rays][256][32].
 extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays) {
   (void)cfg;
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
-  return ((size_t)2 * G_END + (size_t)kBwdBlocks * W_END + n * (kSc + kSf) * 32) * sizeof(float);
+  return ((size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * (kSc + kSf) * 32) * sizeof(float);
 }
 
 extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
@@ -605,7 +772,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.rgb = a->rgb; k.depth = a->depth; k.acc = a->acc; k.sparsity = a->sparsity;
   k.rgb0 = a->rgb0; k.depth0 = a->depth0; k.acc0 = a->acc0; k.sparsity0 = a->sparsity0;
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
-  k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src;
+  k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdWaves - 1) / kFwdWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdWaves), 0, s, k);
   return hip_status(hipGetLastError());
@@ -619,7 +786,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (a->n_rays < 0) return HN_E_SHAPE;
   if (a->n_rays == 0) return HN_OK;
   if (!a->rays || !a->table || !mlp_ok(a->coarse) || !mlp_ok(a->fine)) return HN_E_NULL;
-  if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f || !a->fine_src) return HN_E_NULL;
+  if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f || !a->fine_src || !a->feat)
+    return HN_E_NULL;
   if (!a->d_table || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
@@ -627,7 +795,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
-  float* dfeat = slab + (size_t)kBwdBlocks * W_END;
+  float* dfeat = slab + (size_t)kBwdBlocks * 2 * W_END;
   if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
   if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
   RenderBK k;
@@ -638,18 +806,26 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.Pc = Pc; k.Pf = Pf;
   k.z_coarse = a->z_coarse; k.z_fine = a->z_fine; k.raw_c = a->raw_c; k.raw_f = a->raw_f;
   k.fine_src = a->fine_src;
+  k.feat = a->feat;
   k.dfeat = dfeat;
   k.g_rgb = a->g_rgb; k.g_depth = a->g_depth; k.g_acc = a->g_acc; k.g_sparsity = a->g_sparsity;
   k.g_rgb0 = a->g_rgb0; k.g_depth0 = a->g_depth0; k.g_acc0 = a->g_acc0;
   k.g_sparsity0 = a->g_sparsity0; k.g_raw_f = a->g_raw_f;
   k.d_table = a->d_table;
   k.slab = slab;
-  const size_t lds = (size_t)(W_END + kBwdWaves * kBLds + kGsLds) * sizeof(float);
-  hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kBwdWaves), lds, s, k);
+  const size_t lds = (size_t)kB1Lds * sizeof(float);
+  B1K b;
+  b.B = k.B; b.white = k.white; b.rays = k.rays; b.noise_c = k.noise_c; b.noise_f = k.noise_f;
+  b.Pc = Pc; b.Pf = Pf; b.z_coarse = k.z_coarse; b.z_fine = k.z_fine; b.raw_c = k.raw_c;
+  b.raw_f = k.raw_f; b.feat = k.feat;
+  b.g_rgb = k.g_rgb; b.g_depth = k.g_depth; b.g_acc = k.g_acc; b.g_sparsity = k.g_sparsity;
+  b.g_rgb0 = k.g_rgb0; b.g_depth0 = k.g_depth0; b.g_acc0 = k.g_acc0; b.g_sparsity0 = k.g_sparsity0;
+  b.g_raw_f = k.g_raw_f; b.slab = slab; b.dfeat = dfeat;
+  hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, b);
   if ((st = hip_status(hipGetLastError()))) return st;
   hipLaunchKernelGGL(render_scatter_kernel, dim3((unsigned)((a->n_rays + 3) / 4)), dim3(256), 0, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 255) / 256), dim3(256), 0, s, slab,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(256), 0, s, slab, kBwdBlocks,
                      a->d_coarse, a->d_fine);
   return hip_status(hipGetLastError());
 }

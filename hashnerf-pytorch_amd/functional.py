@@ -201,7 +201,8 @@ class RenderRaysFn(torch.autograd.Function):
     Outputs: rgb, depth, acc, sparsity, rgb0, depth0, acc0, sparsity0, z_std, raw."""
 
     @staticmethod
-    def forward(ctx, cfg: L.HnRenderCfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws):
+    def forward(ctx, cfg: L.HnRenderCfg, keep_feat: bool, rays, t_vals, t_rand, u, noise_c, noise_f,
+                table, *ws):
         L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
         rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                           noise_c, noise_f))
@@ -223,6 +224,11 @@ class RenderRaysFn(torch.autograd.Function):
             setattr(a, k, t.data_ptr())
         fine_src = torch.empty((B, 192), dtype=torch.uint8, device=dev)
         a.fine_src = fine_src.data_ptr()
+        # hash features of every evaluated point, kept for the backward only
+        # when a gradient will be taken (inference skips the 32 KB/ray store)
+        feat = torch.empty((B, L.RENDER_FEAT_PER_RAY) if keep_feat else (0,), dtype=torch.float32,
+                           device=dev)
+        a.feat = feat.data_ptr() if keep_feat else None
         nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
         wsb = _ws(nbytes, dev)
         t0 = TIMER.begin("render_fwd")
@@ -235,14 +241,14 @@ class RenderRaysFn(torch.autograd.Function):
         ctx.has_noise = (noise_c is not None, noise_f is not None)
         ctx.save_for_backward(rays, noise_c if noise_c is not None else rays,
                               noise_f if noise_f is not None else rays, table, out["z_coarse"],
-                              out["z_fine"], out["raw_c"], out["raw_f"], fine_src, *ws)
+                              out["z_fine"], out["raw_c"], out["raw_f"], fine_src, feat, *ws)
         ctx.mark_non_differentiable(out["z_std"])
         return (out["rgb"], out["depth"], out["acc"], out["sparsity"], out["rgb0"], out["depth0"],
                 out["acc0"], out["sparsity0"], out["z_std"], out["raw_f"])
 
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_acc, g_sp, g_rgb0, g_depth0, g_acc0, g_sp0, _g_zstd, g_raw):
-        rays, noise_c, noise_f, table, z_c, z_f, raw_c, raw_f, fine_src, *ws = ctx.saved_tensors
+        rays, noise_c, noise_f, table, z_c, z_f, raw_c, raw_f, fine_src, feat, *ws = ctx.saved_tensors
         noise_c = noise_c if ctx.has_noise[0] else None
         noise_f = noise_f if ctx.has_noise[1] else None
         B = rays.shape[0]
@@ -263,6 +269,7 @@ class RenderRaysFn(torch.autograd.Function):
             keep.append(t)
             setattr(a, k, None if t is None else t.data_ptr())
         a.fine_src = fine_src.data_ptr()
+        a.feat = feat.data_ptr()
         a.d_coarse = L.make_mlp_grad(dws[:5])
         a.d_fine = L.make_mlp_grad(dws[5:])
         nbytes = L.lib().hn_render_workspace_bytes(ctx.cfg, B)
@@ -270,7 +277,7 @@ class RenderRaysFn(torch.autograd.Function):
         t0 = TIMER.begin("render_bwd")
         L.check(L.lib().hn_render_bwd(ctx.cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_bwd")
         TIMER.end("render_bwd", t0)
-        return (None, None, None, None, None, None, None, d_table, *dws)
+        return (None, None, None, None, None, None, None, None, d_table, *dws)
 
 
 class TVFn(torch.autograd.Function):
@@ -339,5 +346,7 @@ def make_render_cfg(grid: L.HnGrid, white_bkgd: bool, lindisp: bool, perturb: bo
 
 def render_rays_fused(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table,
                       coarse_ws: Sequence[torch.Tensor], fine_ws: Sequence[torch.Tensor]):
-    return RenderRaysFn.apply(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table,
+    keep_feat = torch.is_grad_enabled() and any(
+        t.requires_grad for t in (table, *coarse_ws, *fine_ws))
+    return RenderRaysFn.apply(cfg, keep_feat, rays, t_vals, t_rand, u, noise_c, noise_f, table,
                               *coarse_ws, *fine_ws)

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 1
+#define HN_ABI_VERSION 2
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -129,6 +129,8 @@ typedef struct hn_render_cfg {
   int32_t reserved[3];
 } hn_render_cfg;
 
+#define HN_RENDER_FEAT_PER_RAY 8192   /* (64 + 192) points x 16 levels x 2 features */
+
 typedef struct hn_render_fwd_args {
   int64_t n_rays;
   const float* rays;        /* [B][11] = [o3 d3 near far viewdir3] (run_nerf_helpers.py:509-512) */
@@ -150,6 +152,9 @@ typedef struct hn_render_fwd_args {
   float* raw_c;             /* [B][64][4] */
   float* raw_f;             /* [B][192][4] */
   uint8_t* fine_src;        /* [B][192]: coarse index of each fine sample, 255 = importance */
+  float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
+                               evaluated points (MFMA-tile order, opaque); NULL = not kept
+                               (inference); required by hn_render_bwd */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -160,6 +165,7 @@ typedef struct hn_render_bwd_args {
   hn_mlp coarse; hn_mlp fine;
   const float* z_coarse; const float* z_fine; const float* raw_c; const float* raw_f;
   const uint8_t* fine_src;  /* from the forward */
+  const float* feat;        /* from the forward (saved hash features) */
   /* upstream grads (NULL = 0) */
   const float* g_rgb; const float* g_depth; const float* g_acc; const float* g_sparsity;
   const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;

@@ -10,8 +10,10 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 python hashnerf-pytorch_amd/build.py > $OUT/build_$TAG.log 2>&1 || { echo "build failed"; exit 1; }
 timeout -k 10 600 python -m pytest tests -m gpu -q -rf > $OUT/pytest_gpu_$TAG.log 2>&1
-echo "pytest rc=$?" | tee -a $OUT/pytest_gpu_$TAG.log
+RC=$?
+echo "pytest rc=$RC" | tee -a $OUT/pytest_gpu_$TAG.log
 tail -4 $OUT/pytest_gpu_$TAG.log
+[ $RC -le 1 ] || exit $RC     # abort / segfault / timeout: nothing more on the GPU
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 && \
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err && \
 cat $OUT/bench_$TAG.json && \

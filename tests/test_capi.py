@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(hn):
     for n in names:
         assert hasattr(lib, n), n
         assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
-    assert lib.hn_abi_version() == 1
+    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 2
 
 
 def test_struct_sizes_match_header(hn):
@@ -35,6 +35,37 @@ def test_struct_sizes_match_header(hn):
     assert C.sizeof(L.HnMlp) == 5 * 8
     assert C.sizeof(L.HnRenderCfg) == C.sizeof(L.HnGrid) + 8 * 4
     assert L.lib().hn_mlp_workspace_bytes() == L.MLP_PACKED_FLOATS * 4
+
+
+def test_struct_layouts_match_compiled_header(hn, tmp_path):
+    """Every field offset of every ABI struct, as gcc lays out the header,
+    equals the ctypes mirror's offset (catches a field added on one side)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    L = hn._lib
+    structs = {"hn_grid": L.HnGrid, "hn_mlp": L.HnMlp, "hn_mlp_grad": L.HnMlpGrad,
+               "hn_render_cfg": L.HnRenderCfg, "hn_render_fwd_args": L.HnRenderFwdArgs,
+               "hn_render_bwd_args": L.HnRenderBwdArgs, "hn_tv_args": L.HnTvArgs,
+               "hn_radam_tensor": L.HnRadamTensor}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hashnerf_amd.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f in cls._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, cls in structs.items():
+        assert got[(cname, "sizeof")] == C.sizeof(cls), cname
+        for f in cls._fields_:
+            assert got[(cname, f[0])] == getattr(cls, f[0]).offset, (cname, f[0])
 
 
 def test_argument_validation_without_gpu(hn):
