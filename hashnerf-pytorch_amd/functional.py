@@ -291,7 +291,11 @@ class TVFn(torch.autograd.Function):
         a.log2_hashmap_size = int(log2T)
         for l, c in enumerate(cubes):
             a.cube[l] = int(c)
-        mv = min_vertex.to(device=table.device, dtype=torch.int32).contiguous()
+        mv = min_vertex.to(dtype=torch.int32).contiguous()
+        if mv.device.type == "cpu":            # no host stall: pinned + async copy
+            mv = mv.pin_memory().to(table.device, non_blocking=True)
+        else:
+            mv = mv.to(table.device)
         a.min_vertex = mv.data_ptr()
         a.table = table.data_ptr()
         tv = torch.empty(table.shape[0], dtype=torch.float32, device=table.device)

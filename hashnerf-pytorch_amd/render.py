@@ -89,6 +89,20 @@ def sample_pdf(bins, weights, N_samples, det=False, pytest=False):
     return HF.sample_pdf(bins, weights, u)
 
 
+_LINSPACE = {}
+
+
+def _linspace_cached(n, dev):
+    """torch.linspace(0, 1, n) made on the CPU as the reference does (:514),
+    copied to the device once (a per-call pageable copy would stall the
+    host on every training step)."""
+    key = (n, str(dev))
+    t = _LINSPACE.get(key)
+    if t is None:
+        t = _LINSPACE[key] = torch.linspace(0., 1., steps=n).to(dev)
+    return t
+
+
 def _draw(shape, dev, pytest, fn):
     if pytest:
         np.random.seed(0)
@@ -115,7 +129,7 @@ def render_rays(ray_batch, network_fn, network_query_fn, N_samples, embed_fn=Non
     dev = ray_batch.device
     if _fusable(ray_batch, network_fn, network_query_fn, N_samples, N_importance, network_fine):
         emb = network_query_fn.embed_fn
-        t_vals = torch.linspace(0., 1., steps=N_samples).to(dev)
+        t_vals = _linspace_cached(N_samples, dev)
         t_rand = _draw((B, N_samples), dev, pytest, torch.rand) if perturb > 0. else None
         if perturb == 0.:
             if pytest:
@@ -215,7 +229,7 @@ def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far
         ret = render_rays(rays_[i:i + chunk], **kwargs)
         for k in ret:
             all_ret.setdefault(k, []).append(ret[k])
-    all_ret = {k: torch.cat(v, 0) for k, v in all_ret.items()}
+    all_ret = {k: (v[0] if len(v) == 1 else torch.cat(v, 0)) for k, v in all_ret.items()}
     for k in all_ret:
         all_ret[k] = torch.reshape(all_ret[k], list(sh[:-1]) + list(all_ret[k].shape[1:]))
     k_extract = ["rgb_map", "depth_map", "acc_map"]
