@@ -228,6 +228,10 @@ HN_DEV double shfl_from(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+HN_DEV uint32_t shfl_from(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
 template <typename T>
 HN_DEV T wave_sum(T v) {
   const int l = lane_id();

@@ -42,25 +42,6 @@ struct RenderK {
   float* feat;    // [B][8 tiles][1024] saved features or NULL
 };
 
-struct RenderBK {
-  GridArgs g;
-  int white;
-  int64_t B;
-  const float* rays;
-  const float* noise_c;
-  const float* noise_f;
-  const float* table;
-  const float* Pc;
-  const float* Pf;
-  const float *z_coarse, *z_fine, *raw_c, *raw_f;
-  const uint8_t* fine_src;
-  const float* feat;   // [B][8 tiles][1024] features saved by the forward
-  const float *g_rgb, *g_depth, *g_acc, *g_sparsity, *g_rgb0, *g_depth0, *g_acc0, *g_sparsity0;
-  const float* g_raw_f;
-  float* d_table;
-  float* slab;    // [kBwdBlocks][2][W_END]: per-block dW (coarse | fine)
-  float* dfeat;   // [B][64 + 192][32]: d loss / d feature per evaluated point
-};
 
 // Arguments of the backward MLP kernel (kept lean: every field lives in SGPRs).
 struct B1K {
@@ -74,7 +55,11 @@ struct B1K {
   const float *g_rgb, *g_depth, *g_acc, *g_sparsity, *g_rgb0, *g_depth0, *g_acc0, *g_sparsity0;
   const float* g_raw_f;
   float* slab;
-  float* dfeat;
+  float* dfeat;         // [B][64][32] coarse-pass feature grads ([f][level] per point)
+  // fine kernel: trilinear backward + scatter into the table gradient
+  GridArgs g;
+  const uint8_t* fine_src;
+  float* d_table;
 };
 
 struct Ray {
@@ -355,8 +340,8 @@ HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
 
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
-HN_DEV void b1_tile(const float* __restrict__ P, float* X, const f32x16& feat, const f32x16 c0sh[2],
-                    float4 dr, DW& dw, float* __restrict__ dst) {
+HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat, const f32x16 c0sh[2],
+                      float4 dr, DW& dw) {
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
   const int p = lane & 31, h = lane >> 5, i = lane & 31;
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
@@ -448,20 +433,134 @@ HN_DEV void b1_tile(const float* __restrict__ P, float* X, const f32x16& feat, c
   dw.s0[0] = wgrad(X, kRC0 + i, kRF + i, dw.s0[0], lane);
   dw.s0[1] = wgrad(X, kRC0 + 32 + i, kRF + i, dw.s0[1], lane);
   const f32x16 dfeat = gemm<32>(P, G_B0, 0, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
-  // per-point feature gradient stored [point][feature f][level] for the
-  // scatter kernel (lane half h holds levels tile_level(m, h))
+  lds_fence_wave();                             // image reads done before any later writes
+  return dfeat;
+}
+
+// Scatter of one fine tile's table gradient (embedding_dense_backward of
+// hash_encoding.py:106 + trilinear backward).  A fine sample that is one of
+// the 64 coarse samples (fine_src < 64) is the same point in both passes: its
+// coarse-pass feature grads (written by the coarse kernel) are added first,
+// so every unique point is scattered once (25 % fewer atomics).
+//
+// Lane layout: 16 points per pass, 4 lanes per point = (x offset i, feature f).
+// One atomic wave-instruction then covers corners (0,j,k) and (1,j,k) of both
+// features of 16 points: h(x+1) differs from h(x) only in low bits (prime 1
+// on x), so 7/8 of the x-pairs fall in one 64-byte segment and the four dwords
+// of a point go out as ~1 memory request instead of 2 (the float-atomic path
+// is request-rate bound for random rows).  Consecutive points are consecutive
+// samples along the ray; runs inside one voxel are summed first (segmented
+// suffix sum over points) and only the run head issues atomics.
+HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
+                            const float pt[3], const float xc[3], uint32_t l, float gl, int lane) {
+  const int pp = lane >> 2, xi = (lane >> 1) & 1, f = lane & 1;
+  const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
+  uint32_t cell[3];
+  float w[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float q = (xc[a] - g.bmin[a]) / gs[a];
+    const int32_t i = (int32_t)floorf(q);
+    const float vmin = (float)i * gs[a] + g.bmin[a];
+    const float vmax = vmin + gs[a];
+    w[a] = (pt[a] - vmin) / (vmax - vmin);
+    cell[a] = (uint32_t)i;
+  }
+  const uint32_t mask = (1u << g.log2T) - 1u;
+  const uint32_t hx = cell[0] + (uint32_t)xi;
+  const uint32_t y0 = cell[1] * kPrimeY, y1 = (cell[1] + 1u) * kPrimeY;
+  const uint32_t z0 = cell[2] * kPrimeZ, z1 = (cell[2] + 1u) * kPrimeZ;
+  // d feat / d e_c = ((g * fz) * fy) * fx  (trilerp_bwd order), c = 4*xi + jk
+  const float fx = xi ? w[0] : 1.f - w[0];
+  const float gz0 = gl * (1.f - w[2]), gz1 = gl * w[2];
+  float cv[4];
+  cv[0] = (gz0 * (1.f - w[1])) * fx;   // j=0 k=0
+  cv[1] = (gz1 * (1.f - w[1])) * fx;   // j=0 k=1
+  cv[2] = (gz0 * w[1]) * fx;           // j=1 k=0
+  cv[3] = (gz1 * w[1]) * fx;           // j=1 k=1
+  const int up = lane >= 4 ? lane - 4 : lane;
+  const uint32_t q0 = shfl_from(cell[0], up), q1 = shfl_from(cell[1], up), q2 = shfl_from(cell[2], up);
+  const bool head = pp == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
+  const uint64_t hm = __ballot(head);
+  uint32_t pm = 0;                                  // one head bit per point
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pm |= (uint32_t)((hm >> (4 * j)) & 1u) << j;
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
+    if (!__any(same)) break;
+    const int dn = lane + 4 * d < 64 ? lane + 4 * d : lane;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float o = shfl_from(cv[c], dn);
+      if (same) cv[c] += o;
+    }
+  }
+#if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
+  if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
+#else
+  if (head) {
+    const uint32_t row0 = l << g.log2T;
+    const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
+                            (hx ^ y1 ^ z1) & mask};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
+                                            (row0 + hh[c]) * 8u + 4u * f);
+      atomic_add_f32(dst, cv[c]);
+    }
+  }
+#endif
+}
+
+HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r, int64_t ray, int qbase,
+                         const f32x16& dfeat) {
+  const int lane = lane_id();
+  const int p = lane & 31, h = lane >> 5;
+  float* T = X + kRF * kXS;                     // [32 points][kXS]: [feature][level]
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     const int l = h ? tile_level(m, 1) : tile_level(m, 0);
-    dst[l] = dfeat[2 * m];
-    dst[16 + l] = dfeat[2 * m + 1];
+    T[p * kXS + l] = dfeat[2 * m];
+    T[p * kXS + 16 + l] = dfeat[2 * m + 1];
   }
-  lds_fence_wave();                             // image reads done before the next tile's writes
+  lds_fence_wave();
+  const int pp = lane >> 2, f = lane & 1;
+#pragma unroll 1
+  for (int grp = 0; grp < 2; ++grp) {
+    const int q = qbase + 16 * grp + pp;
+    float pt[3], xc[3];
+    ray_point(r, k.z_fine[ray * kSf + q], pt);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
+    float gl[16];
+    const f32x4* src4 = reinterpret_cast<const f32x4*>(T + (16 * grp + pp) * kXS + 16 * f);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 v = src4[c];
+      gl[4 * c] = v.x; gl[4 * c + 1] = v.y; gl[4 * c + 2] = v.z; gl[4 * c + 3] = v.w;
+    }
+    const int src = k.fine_src[ray * kSf + q];
+    if (src < kSc) {
+      const float4* dc = reinterpret_cast<const float4*>(k.dfeat + ((size_t)ray * kSc + src) * 32 + 16 * f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 v = dc[c];
+        gl[4 * c] += v.x; gl[4 * c + 1] += v.y; gl[4 * c + 2] += v.z; gl[4 * c + 3] += v.w;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+      scatter_level_x(k.g, gsl, k.d_table, pt, xc, l, gl[l], lane);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  lds_fence_wave();
 }
 
 // One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
 template <int S>
-HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw) {
+HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, const float* gsl) {
   const int lane = lane_id();
   constexpr int N = S / 64;
   constexpr bool fine = S == kSf;
@@ -516,9 +615,24 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw) {
   f32x16 feat, featn;
   load_feat(k.feat, ray, ctile, lane, feat);
   load_feat(k.feat, ray, ctile + 1, lane, featn);
-  float* dbase = k.dfeat + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0)) * 32;
-  b1_tile(P, X, feat, c0sh, dr[0], dw, dbase + (size_t)(32 * tile0 + p) * 32);
-  b1_tile(P, X, featn, c0sh, dr[1], dw, dbase + (size_t)(32 * (tile0 + 1) + p) * 32);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const f32x16 dfeat = b1_tile(P, X, t ? featn : feat, c0sh, dr[t], dw);
+    const int qbase = 32 * (tile0 + t);
+    if constexpr (fine) {
+      scatter_tile(k, gsl, X, r, ray, qbase, dfeat);
+    } else {
+      // coarse: per-point feature grads [point][feature f][level] for the fine
+      // kernel's scatter (lane half h holds levels tile_level(m, h))
+      float* dst = k.dfeat + ((size_t)ray * kSc + qbase + p) * 32;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int l = h ? tile_level(m, 1) : tile_level(m, 0);
+        dst[l] = dfeat[2 * m];
+        dst[16 + l] = dfeat[2 * m + 1];
+      }
+    }
+  }
 }
 
 // acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS).
@@ -527,6 +641,10 @@ HN_DEV void dw_flush(float* acc, int base, int ld, int n0, int nmax, int k0, int
   accum_block(acc, base, ld, n0, nmax, k0, kmax, d, lane);
 }
 
+// FINE = false: every wave runs coarse units (dW of network_fn, coarse
+// feature grads to k.dfeat).  FINE = true (launched after): fine units with
+// the table-gradient scatter fused in, so its atomics overlap MFMA work.
+template <bool FINE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void render_bwd_kernel(B1K k) {
   extern __shared__ f32x4 smem4[];
@@ -534,24 +652,25 @@ void render_bwd_kernel(B1K k) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   float* X = smem + wave * kRRows * kXS;
-  const bool fine = wave != 0;
+  float* gsl = smem + kB1Lds;
+  if (FINE) stage_grid_sizes(k.g, gsl);
+  __syncthreads();
   DW dw;
 #pragma unroll
   for (int j = 0; j < 2; ++j) dw.c2[j] = dw.c0[j] = dw.s1[j] = dw.s0[j] = zero16();
 #pragma unroll
   for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
-  if (!fine) {
-    for (int64_t ray = blockIdx.x; ray < k.B; ray += gridDim.x) b1_unit<kSc>(k, ray, 0, X, dw);
+  const int64_t w0 = (int64_t)blockIdx.x * kB1Waves + wave, nw = (int64_t)gridDim.x * kB1Waves;
+  if (!FINE) {
+    for (int64_t ray = w0; ray < k.B; ray += nw) b1_unit<kSc>(k, ray, 0, X, dw, gsl);
   } else {
-    const int64_t n_units = 3 * k.B;
-    for (int64_t u = (int64_t)blockIdx.x * 3 + (wave - 1); u < n_units; u += (int64_t)gridDim.x * 3)
-      b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw);
+    for (int64_t u = w0; u < 3 * k.B; u += nw) b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw, gsl);
   }
   // block reduction of the waves' dW (coarse | fine) into LDS, then one slab
   __syncthreads();
-  for (int j = threadIdx.x; j < 2 * W_END; j += blockDim.x) smem[j] = 0.f;
+  for (int j = threadIdx.x; j < W_END; j += blockDim.x) smem[j] = 0.f;
   __syncthreads();
-  float* acc = smem + (fine ? W_END : 0);
+  float* acc = smem;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) dw_flush(acc, W_C2, 64, 0, 3, 32 * kb, 64, dw.c2[kb], lane);
 #pragma unroll
@@ -566,125 +685,8 @@ void render_bwd_kernel(B1K k) {
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) dw_flush(acc, W_S0, 32, 32 * nb, 64, 0, 32, dw.s0[nb], lane);
   __syncthreads();
-  float* slab = k.slab + (size_t)blockIdx.x * 2 * W_END;
-  for (int j = threadIdx.x; j < 2 * W_END; j += blockDim.x) slab[j] = smem[j];
-}
-
-// Scatter of the table gradient, one wave per ray over its 192 UNIQUE points:
-// a fine sample that is one of the 64 coarse samples (fine_src < 64) is the
-// same point in both passes, so its coarse-pass and fine-pass feature grads
-// are summed before the trilinear backward + atomics (25 % fewer atomics).
-// Few registers -> high occupancy to keep many atomics in flight; kept out of
-// the MFMA kernel so the atomics never stall its gathers on vmcnt.
-//
-// Lane layout: 16 points per pass, 4 lanes per point = (x offset i, feature f).
-// One atomic wave-instruction then covers corners (0,j,k) and (1,j,k) of both
-// features of 16 points: h(x+1) differs from h(x) only in low bits (prime 1
-// on x), so 7/8 of the x-pairs fall in one 64-byte segment and the four dwords
-// of a point go out as ~1 memory request instead of 2 (the float-atomic path
-// is request-rate bound for random rows).  Consecutive points are consecutive
-// samples along the ray; runs inside one voxel are summed first (segmented
-// suffix sum over points) and only the run head issues atomics.
-HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
-                            const float pt[3], const float xc[3], uint32_t l, float gl, int pp,
-                            int xi, int f) {
-  const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
-  uint32_t cell[3];
-  float w[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const float q = (xc[a] - g.bmin[a]) / gs[a];
-    const int32_t i = (int32_t)floorf(q);
-    const float vmin = (float)i * gs[a] + g.bmin[a];
-    const float vmax = vmin + gs[a];
-    w[a] = (pt[a] - vmin) / (vmax - vmin);
-    cell[a] = (uint32_t)i;
-  }
-  const uint32_t mask = (1u << g.log2T) - 1u;
-  const uint32_t hx = cell[0] + (uint32_t)xi;
-  const uint32_t y0 = cell[1] * kPrimeY, y1 = (cell[1] + 1u) * kPrimeY;
-  const uint32_t z0 = cell[2] * kPrimeZ, z1 = (cell[2] + 1u) * kPrimeZ;
-  // d feat / d e_c = ((g * fz) * fy) * fx  (trilerp_bwd order), c = 4*xi + jk
-  const float fx = xi ? w[0] : 1.f - w[0];
-  const float gz0 = gl * (1.f - w[2]), gz1 = gl * w[2];
-  float cv[4];
-  cv[0] = (gz0 * (1.f - w[1])) * fx;   // j=0 k=0
-  cv[1] = (gz1 * (1.f - w[1])) * fx;   // j=0 k=1
-  cv[2] = (gz0 * w[1]) * fx;           // j=1 k=0
-  cv[3] = (gz1 * w[1]) * fx;           // j=1 k=1
-  const uint32_t q0 = __shfl_up(cell[0], 4, 64), q1 = __shfl_up(cell[1], 4, 64),
-                 q2 = __shfl_up(cell[2], 4, 64);
-  const bool head = pp == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
-  const uint64_t hm = __ballot(head);
-  uint32_t pm = 0;                                  // one head bit per point
-#pragma unroll
-  for (int j = 0; j < 16; ++j) pm |= (uint32_t)((hm >> (4 * j)) & 1u) << j;
-#pragma unroll
-  for (int d = 1; d < 16; d <<= 1) {
-    const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
-    if (!__any(same)) break;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float o = __shfl_down(cv[c], 4 * d, 64);
-      if (same) cv[c] += o;
-    }
-  }
-  if (head) {
-    const uint32_t row0 = l << g.log2T;
-    const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
-                            (hx ^ y1 ^ z1) & mask};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
-                                            (row0 + hh[c]) * 8u + 4u * f);
-      atomic_add_f32(dst, cv[c]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void render_scatter_kernel(RenderBK k) {
-  __shared__ float gsl[kGsLds];
-  stage_grid_sizes(k.g, gsl);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int pp = lane >> 2, xi = (lane >> 1) & 1, f = lane & 1;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ray >= k.B) return;
-  Ray r;
-  load_ray(k.rays, ray, r);
-  const float* base = k.dfeat + (size_t)ray * (kSc + kSf) * 32;
-  for (int grp = 0; grp < kSf / 16; ++grp) {
-    const int q = 16 * grp + pp;
-    float pt[3], xc[3];
-    ray_point(r, k.z_fine[ray * kSf + q], pt);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
-    const int src = k.fine_src[ray * kSf + q];
-    float gl[16];
-    const float* df = base + (size_t)(kSc + q) * 32 + 16 * f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float4 v = *reinterpret_cast<const float4*>(df + 4 * t);
-      gl[4 * t] = v.x; gl[4 * t + 1] = v.y; gl[4 * t + 2] = v.z; gl[4 * t + 3] = v.w;
-    }
-    if (src < kSc) {
-      const float* dc = base + (size_t)src * 32 + 16 * f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float4 v = *reinterpret_cast<const float4*>(dc + 4 * t);
-        gl[4 * t] += v.x; gl[4 * t + 1] += v.y; gl[4 * t + 2] += v.z; gl[4 * t + 3] += v.w;
-      }
-    }
-#if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
-    if (gl[0] == 1234.5f && gl[1] == -1234.5f) k.d_table[lane] = gl[2];
-#else
-#pragma unroll
-    for (int l = 0; l < 16; ++l) {
-      scatter_level_x(k.g, gsl, k.d_table, pt, xc, l, gl[l], pp, xi, f);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
-  }
+  float* slab = k.slab + ((size_t)blockIdx.x * 2 + (FINE ? 1 : 0)) * W_END;
+  for (int j = threadIdx.x; j < W_END; j += blockDim.x) slab[j] = smem[j];
 }
 
 // dW(coarse) += sum_b slab[b][0], dW(fine) += sum_b slab[b][1].  64
@@ -732,11 +734,11 @@ static bool grad_ok(const hn_mlp_grad& w) {
 using namespace hn;
 
 // Workspace: packed coarse + fine weights | dW slabs [256][2][9344] |
-// per-point feature grads [n_rays][256][32].
+// coarse-pass feature grads [n_rays][64][32].
 extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays) {
   (void)cfg;
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
-  return ((size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * (kSc + kSf) * 32) * sizeof(float);
+  return ((size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32) * sizeof(float);
 }
 
 extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
@@ -798,32 +800,25 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* dfeat = slab + (size_t)kBwdBlocks * 2 * W_END;
   if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
   if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
-  RenderBK k;
-  k.g = make_grid_args(cfg->grid);
-  k.white = cfg->white_bkgd;
+  B1K k;
   k.B = a->n_rays;
-  k.rays = a->rays; k.noise_c = a->noise_c; k.noise_f = a->noise_f; k.table = a->table;
+  k.white = cfg->white_bkgd;
+  k.rays = a->rays; k.noise_c = a->noise_c; k.noise_f = a->noise_f;
   k.Pc = Pc; k.Pf = Pf;
   k.z_coarse = a->z_coarse; k.z_fine = a->z_fine; k.raw_c = a->raw_c; k.raw_f = a->raw_f;
-  k.fine_src = a->fine_src;
   k.feat = a->feat;
-  k.dfeat = dfeat;
   k.g_rgb = a->g_rgb; k.g_depth = a->g_depth; k.g_acc = a->g_acc; k.g_sparsity = a->g_sparsity;
   k.g_rgb0 = a->g_rgb0; k.g_depth0 = a->g_depth0; k.g_acc0 = a->g_acc0;
   k.g_sparsity0 = a->g_sparsity0; k.g_raw_f = a->g_raw_f;
-  k.d_table = a->d_table;
   k.slab = slab;
-  const size_t lds = (size_t)kB1Lds * sizeof(float);
-  B1K b;
-  b.B = k.B; b.white = k.white; b.rays = k.rays; b.noise_c = k.noise_c; b.noise_f = k.noise_f;
-  b.Pc = Pc; b.Pf = Pf; b.z_coarse = k.z_coarse; b.z_fine = k.z_fine; b.raw_c = k.raw_c;
-  b.raw_f = k.raw_f; b.feat = k.feat;
-  b.g_rgb = k.g_rgb; b.g_depth = k.g_depth; b.g_acc = k.g_acc; b.g_sparsity = k.g_sparsity;
-  b.g_rgb0 = k.g_rgb0; b.g_depth0 = k.g_depth0; b.g_acc0 = k.g_acc0; b.g_sparsity0 = k.g_sparsity0;
-  b.g_raw_f = k.g_raw_f; b.slab = slab; b.dfeat = dfeat;
-  hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, b);
+  k.dfeat = dfeat;
+  k.g = make_grid_args(cfg->grid);
+  k.fine_src = a->fine_src;
+  k.d_table = a->d_table;
+  const size_t lds = (size_t)(kB1Lds + kGsLds) * sizeof(float);
+  hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
-  hipLaunchKernelGGL(render_scatter_kernel, dim3((unsigned)((a->n_rays + 3) / 4)), dim3(256), 0, s, k);
+  hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(256), 0, s, slab, kBwdBlocks,
                      a->d_coarse, a->d_fine);
