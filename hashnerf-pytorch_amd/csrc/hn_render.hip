@@ -17,6 +17,8 @@
 #include "hn_mlp.h"
 #include "hn_render.h"
 
+#include <type_traits>
+
 namespace hn {
 
 constexpr int kSc = 64, kNi = 128, kSf = 192;
@@ -326,6 +328,70 @@ HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
   return acc;
 }
 
+// ---- weight-fragment stream ----------------------------------------------
+// A tile's 15 data-path GEMMs read 74 packed A-fragment groups (4 k-steps =
+// one 1-KiB dwordx4 load per wave) in a fixed order, padded to 76 so that a
+// 4-deep ring lines up with the tile period.  The ring keeps the next 4
+// groups (16 MFMAs, ~1000 cycles) in flight across GEMM, tile and unit
+// boundaries: no GEMM starts on an exposed L2 latency at one wave per SIMD.
+struct GemmSeg {
+  int off, ks, ob;
+};
+constexpr GemmSeg kSegs[] = {{G_F0, 16, 0}, {G_F0, 16, 1}, {G_F1, 32, 0}, {G_F2G, 8, 0}, {G_F2G, 8, 1},
+                             {G_F3, 32, 0}, {G_F3, 32, 1}, {G_B4, 4, 0},  {G_B4, 4, 1},  {G_B3, 32, 0},
+                             {G_B3, 32, 1}, {G_B2G, 32, 0}, {G_B1, 8, 0}, {G_B1, 8, 1},  {G_B0, 32, 0}};
+constexpr int kTileGroups = 74, kRing = 4, kTilePeriod = 76;   // 2 pad groups
+constexpr int group_off(int idx) {
+  idx %= kTilePeriod;
+  if (idx >= kTileGroups) idx = 0;              // pad groups re-read group 0
+  for (const GemmSeg& g : kSegs) {
+    const int n = g.ks / 4;
+    if (idx < n) return g.off + (g.ob * n + idx) * 256;
+    idx -= n;
+  }
+  return 0;
+}
+static_assert(group_off(kTileGroups - 1) == G_B0 + 7 * 256, "GEMM sequence");
+
+struct WRing {
+  f32x4 b[kRing];
+};
+
+HN_DEV f32x4 wload(const float* P, int off, int lane) {
+  return *reinterpret_cast<const f32x4*>(opaque_ptr(P) + off + 4 * lane);
+}
+HN_DEV void wring_prime(WRing& w, const float* P, int lane) {
+#pragma unroll
+  for (int j = 0; j < kRing; ++j) w.b[j] = wload(P, group_off(j), lane);
+}
+template <int IDX>
+HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
+  const f32x4 a = w.b[IDX % kRing];
+  w.b[IDX % kRing] = wload(P, group_off(IDX + kRing), lane);
+  return a;
+}
+
+template <int I, int N, typename F>
+HN_DEV void static_for(F&& f) {
+  if constexpr (N > 0) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N - 1>(f);
+  }
+}
+
+// acc += A(groups START .. START + KS/4 of the stream) . B, bval(s) = B operand of k-step s
+template <int KS, int START, typename BF>
+HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
+  static_for<0, KS / 4>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    const f32x4 a = wring_take<START + g>(w, P, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  return acc;
+}
+
 HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -340,38 +406,40 @@ HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
 
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
-HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat, const f32x16 c0sh[2],
-                      float4 dr, DW& dw) {
+HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
+                      const f32x16 c0sh[2], float4 dr, DW& dw) {
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
   const int p = lane & 31, h = lane >> 5, i = lane & 31;
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
   // ---- forward recompute (models.py:151-174) ----
   put_rows(X, kRF, feat, lane);
   f32x16 h0[2];
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob) {
-    h0[ob] = gemm<16>(P, G_F0, ob, zero16(), lane, [&](int s) { return feat[s]; });
-    relu_bits(h0[ob], mh0, ob);
-    put_rows(X, kRH0 + 32 * ob, h0[ob], lane);
-  }
-  const f32x16 s1 = gemm<32>(P, G_F1, 0, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
+  h0[0] = gemm_w<16, 0>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
+  relu_bits(h0[0], mh0, 0);
+  put_rows(X, kRH0, h0[0], lane);
+  h0[1] = gemm_w<16, 4>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
+  relu_bits(h0[1], mh0, 1);
+  put_rows(X, kRH0 + 32, h0[1], lane);
+  const f32x16 s1 = gemm_w<32, 8>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
 #pragma unroll
   for (int r = 0; r < 8; ++r) {                 // geo rows 1..15 -> image rows 16..30
     const int row = row_of(r, h);
     if (row >= 1) X[(kRC0in + 15 + row) * kXS + p] = s1[r];
   }
   f32x16 c0[2];
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob) {
-    c0[ob] = gemm<8>(P, G_F2G, ob, c0sh[ob], lane, [&](int s) { return s1[s]; });
-    relu_bits(c0[ob], mc0, ob);
-    put_rows(X, kRC0 + 32 * ob, c0[ob], lane);
-  }
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob) {
-    f32x16 c1 = gemm<32>(P, G_F3, ob, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
-    relu_bits(c1, mc1, ob);
-    put_rows(X, kRC1 + 32 * ob, c1, lane);
+  c0[0] = gemm_w<8, 16>(wr, P, c0sh[0], lane, [&](int s) { return s1[s]; });
+  relu_bits(c0[0], mc0, 0);
+  put_rows(X, kRC0, c0[0], lane);
+  c0[1] = gemm_w<8, 18>(wr, P, c0sh[1], lane, [&](int s) { return s1[s]; });
+  relu_bits(c0[1], mc0, 1);
+  put_rows(X, kRC0 + 32, c0[1], lane);
+  {
+    f32x16 c1 = gemm_w<32, 20>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    relu_bits(c1, mc1, 0);
+    put_rows(X, kRC1, c1, lane);
+    c1 = gemm_w<32, 28>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    relu_bits(c1, mc1, 1);
+    put_rows(X, kRC1 + 32, c1, lane);
   }
   if (h == 0) {
     X[(kRC2 + 0) * kXS + p] = dr.x;
@@ -385,11 +453,10 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat,
   dw.c2[1] = wgrad(X, rc2, kRC1 + 32 + i, dw.c2[1], lane);
   const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
   f32x16 dc1[2];
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob) {
-    dc1[ob] = gemm<4>(P, G_B4, ob, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
-    mask_bits(dc1[ob], mc1, ob);
-  }
+  dc1[0] = gemm_w<4, 36>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+  dc1[1] = gemm_w<4, 37>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+  mask_bits(dc1[0], mc1, 0);
+  mask_bits(dc1[1], mc1, 1);
   lds_fence_wave();
   // ---- color_net.1 (dc1 image over the c1 rows) ----
   put_rows(X, kRC1, dc1[0], lane);
@@ -401,11 +468,10 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat,
     for (int kb = 0; kb < 2; ++kb)
       dw.c1[2 * nb + kb] = wgrad(X, kRC1 + 32 * nb + i, kRC0 + 32 * kb + i, dw.c1[2 * nb + kb], lane);
   f32x16 dc0[2];
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob) {
-    dc0[ob] = gemm<32>(P, G_B3, ob, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
-    mask_bits(dc0[ob], mc0, ob);
-  }
+  dc0[0] = gemm_w<32, 38>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+  mask_bits(dc0[0], mc0, 0);
+  dc0[1] = gemm_w<32, 46>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+  mask_bits(dc0[1], mc0, 1);
   lds_fence_wave();
   // ---- color_net.0: X = [sh16 | geo15] (dc0 image over the c0 rows) ----
   put_rows(X, kRC0, dc0[0], lane);
@@ -413,7 +479,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat,
   lds_fence_wave();
   dw.c0[0] = wgrad(X, kRC0 + i, kRC0in + i, dw.c0[0], lane);
   dw.c0[1] = wgrad(X, kRC0 + 32 + i, kRC0in + i, dw.c0[1], lane);
-  f32x16 ds1 = gemm<32>(P, G_B2G, 0, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+  f32x16 ds1 = gemm_w<32, 54>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
   // ---- sigma_net.1 (ds1 image over the c1 rows; rows 16..31 are zero) ----
   put_rows(X, kRC1, ds1, lane);
@@ -421,18 +487,19 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat,
   dw.s1[0] = wgrad(X, kRC1 + i, kRH0 + i, dw.s1[0], lane);
   dw.s1[1] = wgrad(X, kRC1 + i, kRH0 + 32 + i, dw.s1[1], lane);
   f32x16 dh0[2];
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob) {
-    dh0[ob] = gemm<8>(P, G_B1, ob, zero16(), lane, [&](int s) { return ds1[s]; });
-    mask_bits(dh0[ob], mh0, ob);
-  }
+  dh0[0] = gemm_w<8, 62>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
+  dh0[1] = gemm_w<8, 64>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
+  mask_bits(dh0[0], mh0, 0);
+  mask_bits(dh0[1], mh0, 1);
   // ---- sigma_net.0 (dh0 image over the c0 rows) ----
   put_rows(X, kRC0, dh0[0], lane);
   put_rows(X, kRC0 + 32, dh0[1], lane);
   lds_fence_wave();
   dw.s0[0] = wgrad(X, kRC0 + i, kRF + i, dw.s0[0], lane);
   dw.s0[1] = wgrad(X, kRC0 + 32 + i, kRF + i, dw.s0[1], lane);
-  const f32x16 dfeat = gemm<32>(P, G_B0, 0, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  const f32x16 dfeat = gemm_w<32, 66>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  (void)wring_take<74>(wr, P, lane);            // pad groups: keep the ring aligned with the tile
+  (void)wring_take<75>(wr, P, lane);
   lds_fence_wave();                             // image reads done before any later writes
   return dfeat;
 }
@@ -443,17 +510,30 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, float* X, const f32x16& feat,
 // coarse-pass feature grads (written by the coarse kernel) are added first,
 // so every unique point is scattered once (25 % fewer atomics).
 //
-// Lane layout: 16 points per pass, 4 lanes per point = (x offset i, feature f).
-// One atomic wave-instruction then covers corners (0,j,k) and (1,j,k) of both
-// features of 16 points: h(x+1) differs from h(x) only in low bits (prime 1
-// on x), so 7/8 of the x-pairs fall in one 64-byte segment and the four dwords
-// of a point go out as ~1 memory request instead of 2 (the float-atomic path
-// is request-rate bound for random rows).  Consecutive points are consecutive
-// samples along the ray; runs inside one voxel are summed first (segmented
-// suffix sum over points) and only the run head issues atomics.
+// Lane layout: lane = 16 * (2 * xi + f) + point, 16 points per pass.  One
+// atomic wave-instruction covers corners (0,j,k) and (1,j,k) of both features
+// of 16 points: h(x+1) differs from h(x) only in low bits (prime 1 on x), so
+// 7/8 of the x-pairs fall in one 64-byte segment and the four dwords of a
+// point go out as ~1 memory request instead of 2 (the float-atomic path is
+// request-rate bound for random rows).  Points are consecutive samples along
+// the ray and sit along a 16-lane DPP row, so a run of samples inside one
+// voxel is summed by a segmented suffix sum of row shifts (no LDS round
+// trips, no branches) and only the run head issues atomics.
+template <int CTRL>
+HN_DEV uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+HN_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf,
+                                                    false));
+}
+constexpr int kRowShr1 = 0x111;              // lane i <- lane i-1 within its row
+template <int D> constexpr int kRowShl = 0x100 + D;   // lane i <- lane i+D within its row
+
 HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
                             const float pt[3], const float xc[3], uint32_t l, float gl, int lane) {
-  const int pp = lane >> 2, xi = (lane >> 1) & 1, f = lane & 1;
+  const int pp = lane & 15, f = (lane >> 4) & 1, xi = lane >> 5;
   const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
   uint32_t cell[3];
   float w[3];
@@ -478,24 +558,23 @@ HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restri
   cv[1] = (gz1 * (1.f - w[1])) * fx;   // j=0 k=1
   cv[2] = (gz0 * w[1]) * fx;           // j=1 k=0
   cv[3] = (gz1 * w[1]) * fx;           // j=1 k=1
-  const int up = lane >= 4 ? lane - 4 : lane;
-  const uint32_t q0 = shfl_from(cell[0], up), q1 = shfl_from(cell[1], up), q2 = shfl_from(cell[2], up);
+  const uint32_t q0 = dpp_u<kRowShr1>(cell[0]), q1 = dpp_u<kRowShr1>(cell[1]),
+                 q2 = dpp_u<kRowShr1>(cell[2]);
   const bool head = pp == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
-  const uint64_t hm = __ballot(head);
-  uint32_t pm = 0;                                  // one head bit per point
-#pragma unroll
-  for (int j = 0; j < 16; ++j) pm |= (uint32_t)((hm >> (4 * j)) & 1u) << j;
-#pragma unroll
-  for (int d = 1; d < 16; d <<= 1) {
+  const uint32_t pm = (uint32_t)__ballot(head) & 0xffffu;   // every row sees the same points
+  // lane p absorbs lane p+d iff no run starts in (p, p+d]
+  auto absorb = [&](auto dc, int d) {
     const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
-    if (!__any(same)) break;
-    const int dn = lane + 4 * d < 64 ? lane + 4 * d : lane;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float o = shfl_from(cv[c], dn);
-      if (same) cv[c] += o;
+      const float o = dpp_f<decltype(dc)::value>(cv[c]);
+      cv[c] = same ? cv[c] + o : cv[c];
     }
-  }
+  };
+  absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
+  absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
+  absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
+  absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
 #if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
   if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
 #else
@@ -517,6 +596,28 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
                          const f32x16& dfeat) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
+  const int pp = lane & 15, f = (lane >> 4) & 1;
+  // every global load of the phase is issued before its first atomic: a load
+  // behind outstanding atomics would wait for all of them (in-order vmcnt)
+  float zq[2], glc[2][16];
+  int srcq[2];
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const int q = qbase + 16 * grp + pp;
+    zq[grp] = k.z_fine[ray * kSf + q];
+    srcq[grp] = k.fine_src[ray * kSf + q];
+  }
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    const bool twin = srcq[grp] < kSc;
+    const float4* dc = reinterpret_cast<const float4*>(
+        k.dfeat + ((size_t)ray * kSc + (twin ? srcq[grp] : 0)) * 32 + 16 * f);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 v = twin ? dc[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      glc[grp][4 * c] = v.x; glc[grp][4 * c + 1] = v.y; glc[grp][4 * c + 2] = v.z; glc[grp][4 * c + 3] = v.w;
+    }
+  }
   float* T = X + kRF * kXS;                     // [32 points][kXS]: [feature][level]
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
@@ -525,12 +626,10 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
     T[p * kXS + 16 + l] = dfeat[2 * m + 1];
   }
   lds_fence_wave();
-  const int pp = lane >> 2, f = lane & 1;
-#pragma unroll 1
+#pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
-    const int q = qbase + 16 * grp + pp;
     float pt[3], xc[3];
-    ray_point(r, k.z_fine[ray * kSf + q], pt);
+    ray_point(r, zq[grp], pt);
 #pragma unroll
     for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
     float gl[16];
@@ -538,21 +637,15 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const f32x4 v = src4[c];
-      gl[4 * c] = v.x; gl[4 * c + 1] = v.y; gl[4 * c + 2] = v.z; gl[4 * c + 3] = v.w;
-    }
-    const int src = k.fine_src[ray * kSf + q];
-    if (src < kSc) {
-      const float4* dc = reinterpret_cast<const float4*>(k.dfeat + ((size_t)ray * kSc + src) * 32 + 16 * f);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float4 v = dc[c];
-        gl[4 * c] += v.x; gl[4 * c + 1] += v.y; gl[4 * c + 2] += v.z; gl[4 * c + 3] += v.w;
-      }
+      // fine-pass grad + coarse twin's grad (zero when not a twin): the order
+      // of the former two-kernel scatter
+      gl[4 * c] = v.x + glc[grp][4 * c]; gl[4 * c + 1] = v.y + glc[grp][4 * c + 1];
+      gl[4 * c + 2] = v.z + glc[grp][4 * c + 2]; gl[4 * c + 3] = v.w + glc[grp][4 * c + 3];
     }
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
       scatter_level_x(k.g, gsl, k.d_table, pt, xc, l, gl[l], lane);
-      __builtin_amdgcn_sched_barrier(0);
+      if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
   lds_fence_wave();
@@ -560,7 +653,7 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
 
 // One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
 template <int S>
-HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, const float* gsl) {
+HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const float* gsl) {
   const int lane = lane_id();
   constexpr int N = S / 64;
   constexpr bool fine = S == kSf;
@@ -617,7 +710,7 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, const
   load_feat(k.feat, ray, ctile + 1, lane, featn);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const f32x16 dfeat = b1_tile(P, X, t ? featn : feat, c0sh, dr[t], dw);
+    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
     const int qbase = 32 * (tile0 + t);
     if constexpr (fine) {
       scatter_tile(k, gsl, X, r, ray, qbase, dfeat);
@@ -661,10 +754,12 @@ void render_bwd_kernel(B1K k) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
   const int64_t w0 = (int64_t)blockIdx.x * kB1Waves + wave, nw = (int64_t)gridDim.x * kB1Waves;
+  WRing wr;
+  wring_prime(wr, FINE ? k.Pf : k.Pc, lane);
   if (!FINE) {
-    for (int64_t ray = w0; ray < k.B; ray += nw) b1_unit<kSc>(k, ray, 0, X, dw, gsl);
+    for (int64_t ray = w0; ray < k.B; ray += nw) b1_unit<kSc>(k, ray, 0, X, dw, wr, gsl);
   } else {
-    for (int64_t u = w0; u < 3 * k.B; u += nw) b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw, gsl);
+    for (int64_t u = w0; u < 3 * k.B; u += nw) b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw, wr, gsl);
   }
   // block reduction of the waves' dW (coarse | fine) into LDS, then one slab
   __syncthreads();

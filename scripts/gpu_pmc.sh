@@ -11,9 +11,14 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 python hashnerf-pytorch_amd/build.py > $OUT/build_$TAG.log 2>&1 || { echo "build failed"; exit 1; }
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-PASSES=("FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum"
-        "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_F32"
-        "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS")
+# counter groups, one rocprofv3 pass each; PMC_PASSES="A B;C D" overrides
+if [ -n "$PMC_PASSES" ]; then
+  IFS=';' read -r -a PASSES <<< "$PMC_PASSES"
+else
+  PASSES=("FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum"
+          "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_F32"
+          "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS")
+fi
 i=0
 for P in "${PASSES[@]}"; do
   i=$((i+1))
