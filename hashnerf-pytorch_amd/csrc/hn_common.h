@@ -275,15 +275,23 @@ HN_DEV constexpr int tile_level(int m, int h) { return (m & 1) + 4 * (m >> 1) + 
 
 // Order this wave's LDS writes before its later LDS reads of other lanes' data
 // (LDS executes one wave's instructions in order; this pins the compiler).
-HN_DEV void lds_fence_wave() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// Deliberately NOT a memory fence: a wavefront-scope fence also waits for
+// vmcnt(0), i.e. for every outstanding global atomic of the wave -- in the
+// fused scatter kernel that drained the atomic queue at every LDS hand-off.
+HN_DEV void lds_fence_wave() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Hide a uniform pointer's value from the optimiser.  Used at the top of tile
 // loops so hipcc cannot hoist hundreds of loop-invariant weight-fragment loads
 // out of the loop (which blows the register file and spills).
+// The result stays a GLOBAL (address space 1) pointer: a laundered generic
+// pointer turns every load through it into a FLAT load, and a pending FLAT op
+// makes the waitcnt pass wait vmcnt(0) lgkmcnt(0) -- no prefetch distance
+// survives and every outstanding atomic of the wave is drained.
 template <typename T>
 HN_DEV T* opaque_ptr(T* p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  uint64_t v = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+s"(v));
+  return (T*)((__attribute__((address_space(1))) T*)v);
 }
 
 inline int32_t hip_status(hipError_t e) { return e == hipSuccess ? HN_OK : HN_E_HIP + (int32_t)e; }

@@ -17,6 +17,9 @@
 #include "hn_mlp.h"
 #include "hn_render.h"
 
+#include <stdio.h>
+#include <string.h>
+
 #include <type_traits>
 
 namespace hn {
@@ -531,21 +534,30 @@ HN_DEV float dpp_f(float v) {
 constexpr int kRowShr1 = 0x111;              // lane i <- lane i-1 within its row
 template <int D> constexpr int kRowShl = 0x100 + D;   // lane i <- lane i+D within its row
 
-HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restrict__ dtable,
-                            const float pt[3], const float xc[3], uint32_t l, float gl, int lane) {
-  const int pp = lane & 15, f = (lane >> 4) & 1, xi = lane >> 5;
-  const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
-  uint32_t cell[3];
-  float w[3];
+// Voxel of one (point, level): cell corner index and trilinear weights, in
+// the op order of hash_encoding.py:62-72 / :130-140 (exact IEEE divisions).
+HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], const float xc[3], int l,
+                     int32_t cell[3], float w[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    const float q = (xc[a] - g.bmin[a]) / gs[a];
+    const float gs = gsl[3 * l + a];
+    const float q = (xc[a] - g.bmin[a]) / gs;
     const int32_t i = (int32_t)floorf(q);
-    const float vmin = (float)i * gs[a] + g.bmin[a];
-    const float vmax = vmin + gs[a];
+    const float vmin = (float)i * gs + g.bmin[a];
+    const float vmax = vmin + gs;
     w[a] = (pt[a] - vmin) / (vmax - vmin);
-    cell[a] = (uint32_t)i;
+    cell[a] = i;
   }
+}
+
+// One level of the scatter for the 16 points of a pass; v = this lane's
+// point's voxel {cell x, y, z, w x, y, z} (from the compact pass via LDS).
+HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const f32x4 v0, const float2 v1,
+                            uint32_t l, float gl, int lane) {
+  const int pp = lane & 15, f = (lane >> 4) & 1, xi = lane >> 5;
+  const uint32_t cell[3] = {(uint32_t)__float_as_int(v0.x), (uint32_t)__float_as_int(v0.y),
+                            (uint32_t)__float_as_int(v0.z)};
+  const float w[3] = {v0.w, v1.x, v1.y};
   const uint32_t mask = (1u << g.log2T) - 1u;
   const uint32_t hx = cell[0] + (uint32_t)xi;
   const uint32_t y0 = cell[1] * kPrimeY, y1 = (cell[1] + 1u) * kPrimeY;
@@ -562,19 +574,21 @@ HN_DEV void scatter_level_x(const GridArgs& g, const float* gsl, float* __restri
                  q2 = dpp_u<kRowShr1>(cell[2]);
   const bool head = pp == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
   const uint32_t pm = (uint32_t)__ballot(head) & 0xffffu;   // every row sees the same points
-  // lane p absorbs lane p+d iff no run starts in (p, p+d]
-  auto absorb = [&](auto dc, int d) {
-    const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
+  if (pm != 0xffffu) {                     // some run of >= 2 samples in one voxel
+    // lane p absorbs lane p+d iff no run starts in (p, p+d]
+    auto absorb = [&](auto dc, int d) {
+      const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float o = dpp_f<decltype(dc)::value>(cv[c]);
-      cv[c] = same ? cv[c] + o : cv[c];
-    }
-  };
-  absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
-  absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
-  absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
-  absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
+      for (int c = 0; c < 4; ++c) {
+        const float o = dpp_f<decltype(dc)::value>(cv[c]);
+        cv[c] = same ? cv[c] + o : cv[c];
+      }
+    };
+    absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
+    absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
+    absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
+    absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
+  }
 #if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
   if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
 #else
@@ -596,7 +610,7 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
                          const f32x16& dfeat) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
-  const int pp = lane & 15, f = (lane >> 4) & 1;
+  const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
   // every global load of the phase is issued before its first atomic: a load
   // behind outstanding atomics would wait for all of them (in-order vmcnt)
   float zq[2], glc[2][16];
@@ -619,19 +633,34 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
     }
   }
   float* T = X + kRF * kXS;                     // [32 points][kXS]: [feature][level]
+  float* V = X + kRH0 * kXS;                    // [16 levels][16 points][8]: voxel of a pass
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     const int l = h ? tile_level(m, 1) : tile_level(m, 0);
     T[p * kXS + l] = dfeat[2 * m];
     T[p * kXS + 16 + l] = dfeat[2 * m + 1];
   }
-  lds_fence_wave();
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
     float pt[3], xc[3];
     ray_point(r, zq[grp], pt);
 #pragma unroll
     for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
+    // compact pass: lane (row lq, point pp) computes levels lq, lq+4, lq+8, lq+12
+    // once, instead of every (x offset, feature) row repeating the divisions
+    if (grp) lds_fence_wave();                  // previous pass's voxel reads done
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int l = 4 * b + lq;
+      int32_t cell[3];
+      float w[3];
+      voxel_cw(k.g, gsl, pt, xc, l, cell, w);
+      float* dst = V + (l * 16 + pp) * 8;
+      *reinterpret_cast<f32x4*>(dst) = f32x4{__int_as_float(cell[0]), __int_as_float(cell[1]),
+                                              __int_as_float(cell[2]), w[0]};
+      *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
+    }
+    lds_fence_wave();
     float gl[16];
     const f32x4* src4 = reinterpret_cast<const f32x4*>(T + (16 * grp + pp) * kXS + 16 * f);
 #pragma unroll
@@ -644,16 +673,47 @@ HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r,
     }
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
-      scatter_level_x(k.g, gsl, k.d_table, pt, xc, l, gl[l], lane);
+      const float* vs = V + (l * 16 + pp) * 8;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
+      const float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
+      scatter_level_x(k.g, k.d_table, v0, v1, l, gl[l], lane);
       if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
   lds_fence_wave();
 }
 
+// Diagnostic phase timers (HN_PROFILE builds only, scripts/b1_profile.sh):
+// per wave, shader-clock cycles spent in the unit prologue (composite
+// backward, sh, loads), in MLP tiles and in scatter tiles.
+#ifndef HN_PROFILE
+#define HN_PROFILE 0
+#endif
+struct PhaseClock {
+#if HN_PROFILE
+  uint64_t t = 0, unit = 0, mlp = 0, scat = 0, tiles = 0;
+  HN_DEV void start() { t = __builtin_amdgcn_s_memtime(); }
+  HN_DEV void lap(uint64_t& acc) {
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    acc += n - t;
+    t = n;
+  }
+#else
+  HN_DEV void start() {}
+#endif
+};
+#if HN_PROFILE
+#define HN_LAP(pc, field) (pc).lap((pc).field)
+__device__ unsigned long long g_phase[2][8];
+#else
+#define HN_LAP(pc, field) ((void)0)
+#endif
+
 // One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
 template <int S>
-HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const float* gsl) {
+HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const float* gsl,
+                    PhaseClock& pc) {
+  pc.start();
   const int lane = lane_id();
   constexpr int N = S / 64;
   constexpr bool fine = S == kSf;
@@ -710,10 +770,13 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   load_feat(k.feat, ray, ctile + 1, lane, featn);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
+    if (t == 0) HN_LAP(pc, unit);
     const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
+    HN_LAP(pc, mlp);
     const int qbase = 32 * (tile0 + t);
     if constexpr (fine) {
       scatter_tile(k, gsl, X, r, ray, qbase, dfeat);
+      HN_LAP(pc, scat);
     } else {
       // coarse: per-point feature grads [point][feature f][level] for the fine
       // kernel's scatter (lane half h holds levels tile_level(m, h))
@@ -756,11 +819,24 @@ void render_bwd_kernel(B1K k) {
   const int64_t w0 = (int64_t)blockIdx.x * kB1Waves + wave, nw = (int64_t)gridDim.x * kB1Waves;
   WRing wr;
   wring_prime(wr, FINE ? k.Pf : k.Pc, lane);
+  PhaseClock pc;
+#if HN_PROFILE
+  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#endif
   if (!FINE) {
-    for (int64_t ray = w0; ray < k.B; ray += nw) b1_unit<kSc>(k, ray, 0, X, dw, wr, gsl);
+    for (int64_t ray = w0; ray < k.B; ray += nw) b1_unit<kSc>(k, ray, 0, X, dw, wr, gsl, pc);
   } else {
-    for (int64_t u = w0; u < 3 * k.B; u += nw) b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw, wr, gsl);
+    for (int64_t u = w0; u < 3 * k.B; u += nw) b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw, wr, gsl, pc);
   }
+#if HN_PROFILE
+  if (lane == 0) {
+    atomicAdd(&g_phase[FINE][0], (unsigned long long)pc.unit);
+    atomicAdd(&g_phase[FINE][1], (unsigned long long)pc.mlp);
+    atomicAdd(&g_phase[FINE][2], (unsigned long long)pc.scat);
+    atomicAdd(&g_phase[FINE][3], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
+    atomicAdd(&g_phase[FINE][4], 1ull);
+  }
+#endif
   // block reduction of the waves' dW (coarse | fine) into LDS, then one slab
   __syncthreads();
   for (int j = threadIdx.x; j < W_END; j += blockDim.x) smem[j] = 0.f;
@@ -915,6 +991,19 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if ((st = hip_status(hipGetLastError()))) return st;
   hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
+#if HN_PROFILE
+  {
+    unsigned long long ph[2][8];
+    hipStreamSynchronize(s);
+    hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
+    for (int f = 0; f < 2; ++f)
+      fprintf(stderr, "hn_b1_profile %s waves=%llu cycles/wave: unit %.0f mlp %.0f scatter %.0f total %.0f\n",
+              f ? "fine" : "coarse", ph[f][4], (double)ph[f][0] / ph[f][4], (double)ph[f][1] / ph[f][4],
+              (double)ph[f][2] / ph[f][4], (double)ph[f][3] / ph[f][4]);
+    memset(ph, 0, sizeof(ph));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph));
+  }
+#endif
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(256), 0, s, slab, kBwdBlocks,
                      a->d_coarse, a->d_fine);
   return hip_status(hipGetLastError());

@@ -24,7 +24,7 @@ for P in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $OUT/pmc_${TAG}_$i -o pmc -- \
       python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline "$@" > $OUT/pmc_${TAG}_$i.log 2>&1 \
-      || echo "pass $i ($P) failed: $(tail -2 $OUT/pmc_${TAG}_$i.log)"
+      || { echo "pass $i ($P) failed: $(tail -2 $OUT/pmc_${TAG}_$i.log)"; exit 1; }
 done
 python3 - "$OUT" "$TAG" "$*" <<'EOF' | tee $OUT/pmc_$TAG.txt
 import csv, glob, json, sys, collections
@@ -33,9 +33,9 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{out}/pmc_{tag}_*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", r.get("Kernel-Name", ""))
-        if not name.startswith("hn::"):
+        if "hn::" not in name:
             continue
-        key = name.split("(")[0]
+        key = name.split("(")[0].replace("void ", "")
         agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in sorted(agg.items()):
     print(k)
