@@ -709,10 +709,17 @@ __device__ unsigned long long g_phase[2][8];
 #define HN_LAP(pc, field) ((void)0)
 #endif
 
+HN_DEV void wait_flag(int* flag, int need) {
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+    __builtin_amdgcn_s_sleep(8);
+}
+
 // One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
+// Fine units: before the first scatter, wait until the block's coarse wave has
+// published this ray's coarse feature grads (*done >= need)
 template <int S>
 HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const float* gsl,
-                    PhaseClock& pc) {
+                    PhaseClock& pc, int* done = nullptr, int need = 0) {
   pc.start();
   const int lane = lane_id();
   constexpr int N = S / 64;
@@ -775,6 +782,7 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
     HN_LAP(pc, mlp);
     const int qbase = 32 * (tile0 + t);
     if constexpr (fine) {
+      if (t == 0) wait_flag(done, need);
       scatter_tile(k, gsl, X, r, ray, qbase, dfeat);
       HN_LAP(pc, scat);
     } else {
@@ -791,16 +799,59 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   }
 }
 
-// acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS).
-HN_DEV void dw_flush(float* acc, int base, int ld, int n0, int nmax, int k0, int kmax, const f32x16& d,
+// acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS),
+// or = (plain stores) when STORE: every dW element belongs to exactly one
+// (block, lane, register) of the twelve blocks.
+template <bool STORE>
+HN_DEV void dw_block(float* acc, int base, int ld, int n0, int nmax, int k0, int kmax, const f32x16& d,
                      int lane) {
-  accum_block(acc, base, ld, n0, nmax, k0, kmax, d, lane);
+  if constexpr (STORE) {
+    const int i = lane & 31, h = lane >> 5;
+    const int kk = k0 + i;
+    if (kk >= kmax) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + row_of(r, h);
+      if (n < nmax) acc[base + n * ld + kk] = d[r];
+    }
+  } else {
+    accum_block(acc, base, ld, n0, nmax, k0, kmax, d, lane);
+  }
 }
 
-// FINE = false: every wave runs coarse units (dW of network_fn, coarse
-// feature grads to k.dfeat).  FINE = true (launched after): fine units with
-// the table-gradient scatter fused in, so its atomics overlap MFMA work.
-template <bool FINE>
+template <bool STORE>
+HN_DEV void dw_flush(const DW& dw, float* acc, int lane) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) dw_block<STORE>(acc, W_C2, 64, 0, 3, 32 * kb, 64, dw.c2[kb], lane);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      dw_block<STORE>(acc, W_C1, 64, 32 * nb, 64, 32 * kb, 64, dw.c1[2 * nb + kb], lane);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) dw_block<STORE>(acc, W_C0, 31, 32 * nb, 64, 0, 31, dw.c0[nb], lane);
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) dw_block<STORE>(acc, W_S1, 64, 0, 16, 32 * kb, 64, dw.s1[kb], lane);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) dw_block<STORE>(acc, W_S0, 32, 32 * nb, 64, 0, 32, dw.s0[nb], lane);
+}
+
+HN_DEV void dw_zero(DW& dw) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) dw.c2[j] = dw.c0[j] = dw.s1[j] = dw.s0[j] = zero16();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
+}
+
+// One persistent block per CU owns rays blockIdx.x + i * gridDim.x.  Wave 0
+// first runs the block's coarse units (MLP backward of network_fn only) and
+// publishes each ray's coarse feature grads through an LDS counter; then it
+// stores its coarse dW to the block's slab and joins the fine units.  Waves
+// 1-3 (and wave 0 once free) take fine units from an LDS work counter: MLP
+// backward of network_fine + the table-gradient scatter, waiting for the ray's
+// coarse grads (twin merge) before the first atomic.  The fine phase is bound
+// by the memory-side float-atomic rate, so the coarse MLP work runs under it.
+// Every wave that waits, waits on a wave of its own workgroup: co-resident.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void render_bwd_kernel(B1K k) {
   extern __shared__ f32x4 smem4[];
@@ -809,54 +860,57 @@ void render_bwd_kernel(B1K k) {
   const int lane = threadIdx.x & 63;
   float* X = smem + wave * kRRows * kXS;
   float* gsl = smem + kB1Lds;
-  if (FINE) stage_grid_sizes(k.g, gsl);
+  int* sync = reinterpret_cast<int*>(gsl + kGsLds);   // [0] coarse rays done, [1] fine units taken
+  stage_grid_sizes(k.g, gsl);
+  if (threadIdx.x == 0) {
+    sync[0] = 0;
+    sync[1] = 0;
+  }
   __syncthreads();
+  const int64_t nb = gridDim.x;
+  const int n_rays = k.B > (int64_t)blockIdx.x ? (int)((k.B - 1 - blockIdx.x) / nb + 1) : 0;
   DW dw;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) dw.c2[j] = dw.c0[j] = dw.s1[j] = dw.s0[j] = zero16();
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
-  const int64_t w0 = (int64_t)blockIdx.x * kB1Waves + wave, nw = (int64_t)gridDim.x * kB1Waves;
+  dw_zero(dw);
   WRing wr;
-  wring_prime(wr, FINE ? k.Pf : k.Pc, lane);
   PhaseClock pc;
 #if HN_PROFILE
   const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #endif
-  if (!FINE) {
-    for (int64_t ray = w0; ray < k.B; ray += nw) b1_unit<kSc>(k, ray, 0, X, dw, wr, gsl, pc);
-  } else {
-    for (int64_t u = w0; u < 3 * k.B; u += nw) b1_unit<kSf>(k, u / 3, (int)(u % 3), X, dw, wr, gsl, pc);
+  if (wave == 0) {
+    wring_prime(wr, k.Pc, lane);
+    for (int i = 0; i < n_rays; ++i) {
+      b1_unit<kSc>(k, blockIdx.x + i * nb, 0, X, dw, wr, gsl, pc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this ray's feature grads are in L2
+      if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    dw_flush<true>(dw, k.slab + (size_t)blockIdx.x * 2 * W_END, lane);
+    dw_zero(dw);
+  }
+  wring_prime(wr, k.Pf, lane);
+  for (;;) {
+    int u = 0;
+    if (lane == 0) u = atomicAdd(&sync[1], 1);
+    u = __builtin_amdgcn_readfirstlane(u);
+    if (u >= 3 * n_rays) break;
+    b1_unit<kSf>(k, blockIdx.x + (int64_t)(u / 3) * nb, u % 3, X, dw, wr, gsl, pc, &sync[0], u / 3 + 1);
   }
 #if HN_PROFILE
   if (lane == 0) {
-    atomicAdd(&g_phase[FINE][0], (unsigned long long)pc.unit);
-    atomicAdd(&g_phase[FINE][1], (unsigned long long)pc.mlp);
-    atomicAdd(&g_phase[FINE][2], (unsigned long long)pc.scat);
-    atomicAdd(&g_phase[FINE][3], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
-    atomicAdd(&g_phase[FINE][4], 1ull);
+    const int role = wave == 0 ? 0 : 1;
+    atomicAdd(&g_phase[role][0], (unsigned long long)pc.unit);
+    atomicAdd(&g_phase[role][1], (unsigned long long)pc.mlp);
+    atomicAdd(&g_phase[role][2], (unsigned long long)pc.scat);
+    atomicAdd(&g_phase[role][3], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
+    atomicAdd(&g_phase[role][4], 1ull);
   }
 #endif
-  // block reduction of the waves' dW (coarse | fine) into LDS, then one slab
+  // block reduction of the waves' fine dW into LDS, then the block's fine slab
   __syncthreads();
   for (int j = threadIdx.x; j < W_END; j += blockDim.x) smem[j] = 0.f;
   __syncthreads();
-  float* acc = smem;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) dw_flush(acc, W_C2, 64, 0, 3, 32 * kb, 64, dw.c2[kb], lane);
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-      dw_flush(acc, W_C1, 64, 32 * nb, 64, 32 * kb, 64, dw.c1[2 * nb + kb], lane);
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb) dw_flush(acc, W_C0, 31, 32 * nb, 64, 0, 31, dw.c0[nb], lane);
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) dw_flush(acc, W_S1, 64, 0, 16, 32 * kb, 64, dw.s1[kb], lane);
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb) dw_flush(acc, W_S0, 32, 32 * nb, 64, 0, 32, dw.s0[nb], lane);
+  dw_flush<false>(dw, smem, lane);
   __syncthreads();
-  float* slab = k.slab + ((size_t)blockIdx.x * 2 + (FINE ? 1 : 0)) * W_END;
+  float* slab = k.slab + ((size_t)blockIdx.x * 2 + 1) * W_END;
   for (int j = threadIdx.x; j < W_END; j += blockDim.x) slab[j] = smem[j];
 }
 
@@ -986,10 +1040,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.g = make_grid_args(cfg->grid);
   k.fine_src = a->fine_src;
   k.d_table = a->d_table;
-  const size_t lds = (size_t)(kB1Lds + kGsLds) * sizeof(float);
-  hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
-  if ((st = hip_status(hipGetLastError()))) return st;
-  hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
+  const size_t lds = (size_t)(kB1Lds + kGsLds + 4) * sizeof(float);
+  hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
 #if HN_PROFILE
   {
@@ -998,7 +1050,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
     for (int f = 0; f < 2; ++f)
       fprintf(stderr, "hn_b1_profile %s waves=%llu cycles/wave: unit %.0f mlp %.0f scatter %.0f total %.0f\n",
-              f ? "fine" : "coarse", ph[f][4], (double)ph[f][0] / ph[f][4], (double)ph[f][1] / ph[f][4],
+              f ? "waves1-3" : "wave0", ph[f][4], (double)ph[f][0] / ph[f][4], (double)ph[f][1] / ph[f][4],
               (double)ph[f][2] / ph[f][4], (double)ph[f][3] / ph[f][4]);
     memset(ph, 0, sizeof(ph));
     hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph));
