@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 2                 # HN_ABI_VERSION
+ABI_VERSION = 3                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 24064
@@ -60,7 +60,8 @@ class HnRenderFwdArgs(C.Structure):
 class HnRenderBwdArgs(C.Structure):
     _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("noise_c", _P), ("noise_f", _P), ("table", _P),
                 ("coarse", HnMlp), ("fine", HnMlp), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P),
-                ("raw_f", _P), ("fine_src", _P), ("feat", _P), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
+                ("raw_f", _P), ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32),
+                ("reserved", C.c_int32), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
 
@@ -71,6 +72,13 @@ class HnTvArgs(C.Structure):
 
 
 RADAM_MAX_TENSORS = 16
+
+
+class HnRaySampler(C.Structure):
+    _fields_ = [("H", C.c_int32), ("W", C.c_int32), ("crop_y0", C.c_int32), ("crop_x0", C.c_int32),
+                ("crop_h", C.c_int32), ("crop_w", C.c_int32), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("near", C.c_float), ("far", C.c_float),
+                ("seed", C.c_uint64)]
 
 
 class HnRadamTensor(C.Structure):
@@ -100,6 +108,11 @@ SIGNATURES = {
     "hn_tv_fwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P]),
     "hn_tv_bwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P, _P]),
     "hn_radam_step": (C.c_int32, [C.POINTER(HnRadamTensor), C.c_int32, _P]),
+    "hn_sample_rays": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P]),
+    "hn_loss_fwd": (C.c_int32, [_P, _P, _P, _P, _P, C.c_int64, _P, C.c_int32, C.c_float, C.c_float,
+                                C.c_float, _P, _P]),
+    "hn_loss_bwd": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_float, _P,
+                                _P, _P, _P, _P, _P, _P]),
     "hn_render_workspace_bytes": (C.c_size_t, [C.POINTER(HnRenderCfg), C.c_int64]),
     "hn_render_fwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderFwdArgs), _P,
                                   C.c_size_t, _P]),

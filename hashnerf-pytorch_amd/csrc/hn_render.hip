@@ -922,8 +922,16 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
   float s = 0.f;
-  if (e < 2 * W_END)
-    for (int b = grp; b < n_slabs; b += 4) s += slab[(size_t)b * 2 * W_END + e];
+  if (e < 2 * W_END) {
+    // four independent chains keep 4 loads in flight per thread
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = grp;
+    for (; b + 12 < n_slabs; b += 16)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += slab[(size_t)(b + 4 * q) * 2 * W_END + e];
+    for (; b < n_slabs; b += 4) acc[0] += slab[(size_t)b * 2 * W_END + e];
+    s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
   part[grp][threadIdx.x & 63] = s;
   __syncthreads();
   if (grp != 0 || e >= 2 * W_END) return;
@@ -1023,8 +1031,10 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
   float* dfeat = slab + (size_t)kBwdBlocks * 2 * W_END;
-  if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
-  if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
+  if (!a->weights_packed) {
+    if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
+    if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
+  }
   B1K k;
   k.B = a->n_rays;
   k.white = cfg->white_bkgd;

@@ -1,0 +1,190 @@
+// hn_train.hip -- the training-step driver pieces around the fused renderer
+// (run_nerf.py:576-636), so one step is a handful of launches:
+//   * hn_sample_rays: N_rand distinct pixels of one image (without
+//     replacement), their rays (ray_util.py:62-80) packed as the ray batch
+//     render() builds (run_nerf_helpers.py:355-368), and their target colours;
+//   * hn_loss_fwd / hn_loss_bwd: the loss of run_nerf.py:612-636 (with the
+//     data-parallel scaling of train.dp_loss) and its input gradients in
+//     torch autograd's op order, instead of ~25 tiny eager kernels.
+#include "hn_common.h"
+
+namespace hn {
+
+// ---------------------------------------------------------------------------
+// Pixel sampling without replacement: a keyed 4-round Feistel permutation of
+// [0, 2^k) (k even, 2^k >= window size M), restricted to [0, M) by cycle
+// walking, is a bijection of [0, M); sample i is perm(i), so the n samples
+// are distinct for any seed.
+// ---------------------------------------------------------------------------
+HN_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+HN_DEV uint32_t feistel(uint32_t x, int half, uint64_t seed) {
+  const uint32_t mask = (1u << half) - 1u;
+  uint32_t L = x >> half, R = x & mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t key = (uint32_t)(seed >> (16 * r)) ^ (0x9e3779b9u * (uint32_t)(r + 1));
+    const uint32_t F = mix32(R ^ key) & mask;
+    const uint32_t t = R;
+    R = L ^ F;
+    L = t;
+  }
+  return (L << half) | R;
+}
+
+__global__ __launch_bounds__(256) void sample_rays_kernel(hn_ray_sampler s, const float* __restrict__ image,
+                                                          const float* __restrict__ c2w, int64_t n,
+                                                          int half, float* __restrict__ rays,
+                                                          float* __restrict__ target) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t M = (uint32_t)s.crop_h * (uint32_t)s.crop_w;
+  uint32_t x = (uint32_t)i;
+  do {
+    x = feistel(x, half, s.seed);
+  } while (x >= M);
+  const int py = s.crop_y0 + (int)(x / (uint32_t)s.crop_w);
+  const int px = s.crop_x0 + (int)(x % (uint32_t)s.crop_w);
+  // dirs = [(i - cx) / fx, -(j - cy) / fy, -1]; rays_d = sum(dirs * c2w[:3,:3], -1)
+  const float d0 = ((float)px - s.cx) / s.fx;
+  const float d1 = -(((float)py - s.cy) / s.fy);
+  const float d2 = -1.f;
+  float* out = rays + 11 * i;
+  float d[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    d[a] = d0 * c2w[4 * a] + d1 * c2w[4 * a + 1] + d2 * c2w[4 * a + 2];
+    out[a] = c2w[4 * a + 3];
+    out[3 + a] = d[a];
+  }
+  out[6] = s.near;
+  out[7] = s.far;
+  const float nrm = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) out[8 + a] = d[a] / nrm;
+  const float* px3 = image + 3 * ((size_t)py * s.W + px);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) target[3 * i + a] = px3[a];
+}
+
+// ---------------------------------------------------------------------------
+// Loss.  Forward: one workgroup, fp64 accumulation of the reductions (the
+// value is reported, its gradient does not depend on the summation order).
+// ---------------------------------------------------------------------------
+constexpr int kLossThreads = 1024;
+
+__global__ __launch_bounds__(kLossThreads) void loss_fwd_kernel(
+    const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target,
+    const float* __restrict__ sp, const float* __restrict__ sp0, int64_t n, const float* __restrict__ tv,
+    int n_tv, float world, float sparse_w, float tv_w, float* __restrict__ out) {
+  __shared__ double red[4][kLossThreads / 64];
+  double a[4] = {0.0, 0.0, 0.0, 0.0};   // sse, sse0, entropy, tv
+  for (int64_t j = threadIdx.x; j < 3 * n; j += kLossThreads) {
+    const float e = rgb[j] - target[j];
+    a[0] += (double)(e * e);
+    if (rgb0) {
+      const float e0 = rgb0[j] - target[j];
+      a[1] += (double)(e0 * e0);
+    }
+  }
+  for (int64_t j = threadIdx.x; j < n; j += kLossThreads) a[2] += (double)sp[j] + (sp0 ? (double)sp0[j] : 0.0);
+  if (tv)
+    for (int j = threadIdx.x; j < n_tv; j += kLossThreads) a[3] += (double)tv[j];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double v = wave_sum(a[q]);
+    if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < 4; ++q)
+      for (int w = 0; w < kLossThreads / 64; ++w) t[q] += red[q][w];
+    const double N = 3.0 * (double)n;
+    const float mse = (float)(t[0] / N), mse0 = rgb0 ? (float)(t[1] / N) : 0.f;
+    const float ent = (float)t[2];
+    out[0] = (mse + mse0) / world + sparse_w * ent + (tv ? tv_w * (float)t[3] : 0.f);
+    out[1] = mse;
+    out[2] = mse0;
+    out[3] = ent;
+  }
+}
+
+// Backward, op for op as autograd evaluates the eager expression:
+//   (mse + mse0) / world   -> g / world (DivBackward)
+//   mean over 3n            -> (.) / 3n  (MeanBackward: expand, divide by numel)
+//   (x - t) ** 2            -> (.) * (2 * (x - t))  (PowBackward)
+//   sparse_w * sum(sp)      -> g * sparse_w;   tv_w * sum(tv) -> g * tv_w
+__global__ __launch_bounds__(256) void loss_bwd_kernel(
+    const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target, int64_t n,
+    int n_tv, float world, float sparse_w, float tv_w, const float* __restrict__ g_loss,
+    float* __restrict__ g_rgb, float* __restrict__ g_rgb0, float* __restrict__ g_sp, float* __restrict__ g_sp0,
+    float* __restrict__ g_tv) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float g = *g_loss;
+  const float gm = (g / world) / (float)(3 * n);
+  if (j < 3 * n) {
+    g_rgb[j] = gm * (2.f * (rgb[j] - target[j]));
+    if (rgb0) g_rgb0[j] = gm * (2.f * (rgb0[j] - target[j]));
+  }
+  if (j < n) {
+    if (g_sp) g_sp[j] = g * sparse_w;
+    if (g_sp0) g_sp0[j] = g * sparse_w;
+  }
+  if (g_tv && j < n_tv) g_tv[j] = g * tv_w;
+}
+
+}  // namespace hn
+
+using namespace hn;
+
+extern "C" int32_t hn_sample_rays(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
+                                  float* rays, float* target, void* stream) {
+  if (!s) return HN_E_NULL;
+  if (n_rays < 0) return HN_E_SHAPE;
+  if (n_rays == 0) return HN_OK;
+  if (!image || !c2w || !rays || !target) return HN_E_NULL;
+  if (s->H <= 0 || s->W <= 0 || s->crop_h <= 0 || s->crop_w <= 0 || s->crop_y0 < 0 || s->crop_x0 < 0 ||
+      s->crop_y0 + s->crop_h > s->H || s->crop_x0 + s->crop_w > s->W)
+    return HN_E_SHAPE;
+  const uint64_t M = (uint64_t)s->crop_h * (uint64_t)s->crop_w;
+  if ((uint64_t)n_rays > M || M > (1ull << 30)) return HN_E_SHAPE;   // without replacement
+  int bits = 2;
+  while ((1ull << bits) < M) bits += 2;
+  const unsigned blocks = (unsigned)((n_rays + 255) / 256);
+  hipLaunchKernelGGL(sample_rays_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *s, image, c2w, n_rays,
+                     bits / 2, rays, target);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_loss_fwd(const float* rgb, const float* rgb0, const float* target, const float* sp,
+                               const float* sp0, int64_t n_rays, const float* tv, int32_t n_tv, float world,
+                               float sparse_w, float tv_w, float* out, void* stream) {
+  if (n_rays <= 0 || n_tv < 0) return HN_E_SHAPE;
+  if (!rgb || !target || !sp || !out) return HN_E_NULL;
+  if ((rgb0 == nullptr) != (sp0 == nullptr)) return HN_E_NULL;
+  hipLaunchKernelGGL(loss_fwd_kernel, dim3(1), dim3(kLossThreads), 0, (hipStream_t)stream, rgb, rgb0, target, sp,
+                     sp0, n_rays, tv, n_tv, world, sparse_w, tv_w, out);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_loss_bwd(const float* rgb, const float* rgb0, const float* target, int64_t n_rays,
+                               int32_t n_tv, float world, float sparse_w, float tv_w, const float* g_loss,
+                               float* g_rgb, float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv,
+                               void* stream) {
+  if (n_rays <= 0 || n_tv < 0) return HN_E_SHAPE;
+  if (!rgb || !target || !g_loss || !g_rgb) return HN_E_NULL;
+  if ((rgb0 == nullptr) != (g_rgb0 == nullptr)) return HN_E_NULL;
+  const int64_t m = 3 * n_rays > n_tv ? 3 * n_rays : n_tv;
+  const unsigned blocks = (unsigned)((m + 255) / 256);
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rgb, rgb0, target, n_rays,
+                     n_tv, world, sparse_w, tv_w, g_loss, g_rgb, g_rgb0, g_sp, g_sp0, g_tv);
+  return hip_status(hipGetLastError());
+}

@@ -237,6 +237,7 @@ class RenderRaysFn(torch.autograd.Function):
         if DEBUG_KEEP:
             LAST.update({k: out[k] for k in ("z_coarse", "z_fine", "raw_c", "raw_f")})
         ctx.cfg = cfg
+        ctx.wsb = wsb                      # holds the packed weights for the backward
         ctx.set_materialize_grads(False)   # unused outputs => NULL, not zeros (0*inf)
         ctx.has_noise = (noise_c is not None, noise_f is not None)
         ctx.save_for_backward(rays, noise_c if noise_c is not None else rays,
@@ -270,14 +271,90 @@ class RenderRaysFn(torch.autograd.Function):
             setattr(a, k, None if t is None else t.data_ptr())
         a.fine_src = fine_src.data_ptr()
         a.feat = feat.data_ptr()
+        a.weights_packed = 1               # same workspace and weights as the forward
         a.d_coarse = L.make_mlp_grad(dws[:5])
         a.d_fine = L.make_mlp_grad(dws[5:])
         nbytes = L.lib().hn_render_workspace_bytes(ctx.cfg, B)
-        wsb = _ws(nbytes, dev)
+        wsb = ctx.wsb
         t0 = TIMER.begin("render_bwd")
         L.check(L.lib().hn_render_bwd(ctx.cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_bwd")
         TIMER.end("render_bwd", t0)
         return (None, None, None, None, None, None, None, None, d_table, *dws)
+
+
+# --------------------------------------------------------------------------
+# training-step driver (run_nerf.py:576-636)
+# --------------------------------------------------------------------------
+def sample_rays(image, c2w, n_rays, K, near, far, crop, seed):
+    """N_rand distinct pixels of one image (device, no replacement) -> the
+    [n, 11] ray batch render() builds and the [n, 3] target colours.
+    image [H, W, 3], c2w [3, 4] (or [4, 4]) fp32 on the device; crop =
+    (y0, x0, h, w) sampling window; K the 3x3 intrinsics (host numbers)."""
+    L.require_device(image, c2w)
+    image, c2w = image.contiguous(), c2w[:3, :4].contiguous()
+    H, W = image.shape[0], image.shape[1]
+    s = L.HnRaySampler()
+    s.H, s.W = H, W
+    s.crop_y0, s.crop_x0, s.crop_h, s.crop_w = (int(v) for v in crop)
+    s.fx, s.fy, s.cx, s.cy = float(K[0][0]), float(K[1][1]), float(K[0][2]), float(K[1][2])
+    s.near, s.far = float(near), float(far)
+    s.seed = int(seed) & ((1 << 64) - 1)
+    dev = image.device
+    rays = torch.empty((n_rays, 11), dtype=torch.float32, device=dev)
+    target = torch.empty((n_rays, 3), dtype=torch.float32, device=dev)
+    L.check(L.lib().hn_sample_rays(s, L.ptr(image), L.ptr(c2w), n_rays, L.ptr(rays), L.ptr(target),
+                                   L.stream(dev)), "sample_rays")
+    return rays, target
+
+
+class TrainLossFn(torch.autograd.Function):
+    """loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * (sum sp + sum sp0) +
+    tv_w * sum tv (run_nerf.py:612-636 under train.dp_loss's DP rule).
+    Returns (loss, mse, mse0); mse/mse0 carry no gradient."""
+
+    @staticmethod
+    def forward(ctx, rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w):
+        L.require_device(rgb, target, sp)
+        rgb, target, sp = rgb.contiguous(), target.contiguous(), sp.contiguous()
+        rgb0 = None if rgb0 is None else rgb0.contiguous()
+        sp0 = None if sp0 is None else sp0.contiguous()
+        tv = None if tv is None else tv.contiguous()
+        n = rgb.shape[0]
+        out = torch.empty(4, dtype=torch.float32, device=rgb.device)
+        L.check(L.lib().hn_loss_fwd(L.ptr(rgb), L.ptr(rgb0), L.ptr(target), L.ptr(sp), L.ptr(sp0), n,
+                                    L.ptr(tv), 0 if tv is None else tv.numel(), float(world),
+                                    float(sparse_w), float(tv_w), L.ptr(out), L.stream(rgb.device)),
+                "loss_fwd")
+        ctx.save_for_backward(rgb, rgb0 if rgb0 is not None else rgb, target)
+        ctx.has = (rgb0 is not None, sp0 is not None, tv is not None)
+        ctx.n_tv = 0 if tv is None else tv.numel()
+        ctx.consts = (float(world), float(sparse_w), float(tv_w))
+        mse, mse0 = out[1], out[2]
+        ctx.mark_non_differentiable(mse, mse0)
+        return out[0], mse, mse0
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_mse, _g_mse0):
+        rgb, rgb0, target = ctx.saved_tensors
+        has0, has_sp0, has_tv = ctx.has
+        rgb0 = rgb0 if has0 else None
+        n = rgb.shape[0]
+        dev = rgb.device
+        g = (g_loss if g_loss is not None else torch.ones((), device=dev)).contiguous()
+        g_rgb = torch.empty_like(rgb)
+        g_rgb0 = torch.empty_like(rgb) if has0 else None
+        g_sp = torch.empty(n, dtype=torch.float32, device=dev)
+        g_sp0 = torch.empty(n, dtype=torch.float32, device=dev) if has_sp0 else None
+        g_tv = torch.empty(ctx.n_tv, dtype=torch.float32, device=dev) if has_tv else None
+        world, sparse_w, tv_w = ctx.consts
+        L.check(L.lib().hn_loss_bwd(L.ptr(rgb), L.ptr(rgb0), L.ptr(target), n, ctx.n_tv, world, sparse_w,
+                                    tv_w, L.ptr(g), L.ptr(g_rgb), L.ptr(g_rgb0), L.ptr(g_sp),
+                                    L.ptr(g_sp0), L.ptr(g_tv), L.stream(dev)), "loss_bwd")
+        return g_rgb, g_rgb0, None, g_sp, g_sp0, g_tv, None, None, None
+
+
+def train_loss(rgb, rgb0, target, sp, sp0, tv=None, world=1, sparse_w=0.0, tv_w=0.0):
+    return TrainLossFn.apply(rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w)
 
 
 class TVFn(torch.autograd.Function):

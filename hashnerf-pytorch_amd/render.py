@@ -224,6 +224,16 @@ def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far
     rays_ = torch.cat([rays_o, rays_d, near, far], -1)
     if use_viewdirs:
         rays_ = torch.cat([rays_, viewdirs], -1)
+    return render_ray_batch(rays_, sh[:-1], chunk, **kwargs)
+
+
+def render_ray_batch(rays_, out_shape, chunk=1024 * 32, **kwargs):
+    """The chunk loop + output assembly of render() (run_nerf_helpers.py:370-392)
+    over an already built [N, 8 or 11] ray batch (e.g. from the device sampler).
+    render()-level keywords of a render_kwargs dict (ndc, near, far,
+    use_viewdirs, c2w_staticcam) are already baked into the batch."""
+    for k in ("ndc", "near", "far", "use_viewdirs", "c2w_staticcam"):
+        kwargs.pop(k, None)
     all_ret = {}
     for i in range(0, rays_.shape[0], chunk):
         ret = render_rays(rays_[i:i + chunk], **kwargs)
@@ -231,7 +241,7 @@ def render(H, W, K, chunk=1024 * 32, rays=None, c2w=None, ndc=True, near=0., far
             all_ret.setdefault(k, []).append(ret[k])
     all_ret = {k: (v[0] if len(v) == 1 else torch.cat(v, 0)) for k, v in all_ret.items()}
     for k in all_ret:
-        all_ret[k] = torch.reshape(all_ret[k], list(sh[:-1]) + list(all_ret[k].shape[1:]))
+        all_ret[k] = torch.reshape(all_ret[k], list(out_shape) + list(all_ret[k].shape[1:]))
     k_extract = ["rgb_map", "depth_map", "acc_map"]
     return [all_ret[k] for k in k_extract] + [{k: all_ret[k] for k in all_ret if k not in k_extract}]
 

@@ -22,10 +22,11 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from . import functional as HF
 from .create import create_nerf
 from .loss import tv_loss_levels
 from .rays import bbox_for_blender, blender_cameras, blender_intrinsics
-from .render import img2mse, mse2psnr, render
+from .render import img2mse, mse2psnr, render, render_ray_batch
 
 
 def dp_loss(mse_fine, mse_coarse, entropy_sum, world, sparse_loss_weight, tv=None,
@@ -89,10 +90,26 @@ class SyntheticBlender:
         self.i_train = torch.arange(n)
 
 
+def _step_seed(seed, rank, step):
+    """64-bit splitmix of (seed, rank, step): the device sampler's key."""
+    x = (seed * 0x9E3779B97F4A7C15 + rank * 0xBF58476D1CE4E5B9 + step * 0x94D049BB133111EB) & (2 ** 64 - 1)
+    x ^= x >> 30
+    x = (x * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+    x ^= x >> 27
+    x = (x * 0x94D049BB133111EB) & (2 ** 64 - 1)
+    return x ^ (x >> 31)
+
+
 class Trainer:
-    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0):
+    """fused=True (default): device ray sampler (hn_sample_rays) + fused loss
+    (hn_loss_fwd/bwd) around the fused renderer -- a handful of launches per
+    step.  fused=False: the same step in eager torch ops (randperm sampling,
+    img2mse, sums), kept as the op-for-op rendition of run_nerf.py."""
+
+    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0, fused=True):
         self.args, self.data, self.device = args, data, torch.device(device)
         self.rank, self.world = rank, world
+        self.seed, self.fused = seed, fused
         args.bounding_box = data.bounding_box
         torch.manual_seed(seed)                      # identical init on every rank
         (self.kw_train, self.kw_test, self.start, self.grad_vars,
@@ -111,6 +128,7 @@ class Trainer:
         cj, ci = torch.meshgrid(torch.arange(H // 2 - dH, H // 2 + dH, device=self.device),
                                 torch.arange(W // 2 - dW, W // 2 + dW, device=self.device), indexing="ij")
         self.coords_crop = torch.stack([cj, ci], -1).reshape(-1, 2)
+        self.crop = (H // 2 - dH, W // 2 - dW, 2 * dH, 2 * dW)
 
     def sample_rays(self, i: int):
         """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
@@ -145,11 +163,26 @@ class Trainer:
 
     def step(self, i: int):
         a = self.args
-        batch_rays, target = self.sample_rays(i)
-        rgb, depth, acc, extras = render(self.data.H, self.data.W, self.data.K, chunk=a.chunk,
-                                         rays=batch_rays, retraw=True, near=2., far=6., **self.kw_train)
         self.optimizer.zero_grad(set_to_none=True)
-        loss, mse = self.loss_fn(rgb, extras, target, i)
+        if self.fused:
+            d = self.data
+            img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
+            crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
+            rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
+                                          _step_seed(self.seed, self.rank, i))
+            rgb, depth, acc, extras = render_ray_batch(rays, (a.N_rand,), chunk=a.chunk, retraw=True,
+                                                       **self.kw_train)
+            tv = None
+            if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
+                tv = tv_loss_levels(self.embed_fn, generator=self.cpu_gen)
+            loss, mse, _ = HF.train_loss(rgb, extras.get("rgb0"), target, extras["sparsity_loss"],
+                                         extras.get("sparsity_loss0"), tv, self.world, a.sparse_loss_weight,
+                                         a.tv_loss_weight)
+        else:
+            batch_rays, target = self.sample_rays(i)
+            rgb, depth, acc, extras = render(self.data.H, self.data.W, self.data.K, chunk=a.chunk,
+                                             rays=batch_rays, retraw=True, near=2., far=6., **self.kw_train)
+            loss, mse = self.loss_fn(rgb, extras, target, i)
         loss.backward()
         self.allreduce_grads()
         self.optimizer.step()

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 2
+#define HN_ABI_VERSION 3
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -166,6 +166,9 @@ typedef struct hn_render_bwd_args {
   const float* z_coarse; const float* z_fine; const float* raw_c; const float* raw_f;
   const uint8_t* fine_src;  /* from the forward */
   const float* feat;        /* from the forward (saved hash features) */
+  int32_t weights_packed;   /* nonzero: `workspace` is the one hn_render_fwd used and the weights
+                               are unchanged since, so its packed MFMA copies are reused */
+  int32_t reserved;
   /* upstream grads (NULL = 0) */
   const float* g_rgb; const float* g_depth; const float* g_acc; const float* g_sparsity;
   const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;
@@ -209,6 +212,36 @@ typedef struct hn_radam_tensor {
   int32_t reserved;
 } hn_radam_tensor;
 int32_t hn_radam_step(const hn_radam_tensor* ts, int32_t n_tensors, void* stream);
+
+/* ---- L5 training-step driver (run_nerf.py:576-636) -----------------------
+ * Device ray sampler: n_rays DISTINCT pixels of one training image drawn
+ * without replacement (np.random.choice(..., replace=False) at
+ * run_nerf.py:595; here a seeded Feistel permutation of the crop window with
+ * cycle walking), the rays of ray_util.py:62-80 for them, and their target
+ * colours.  rays[n][11] = [o3 d3 near far viewdir3] (the ray batch render()
+ * builds, run_nerf_helpers.py:355-368); target[n][3]. */
+typedef struct hn_ray_sampler {
+  int32_t H, W;                        /* image size */
+  int32_t crop_y0, crop_x0, crop_h, crop_w;   /* sampling window (precrop, :584-593) */
+  float fx, fy, cx, cy;                /* intrinsics K */
+  float near, far;
+  uint64_t seed;                       /* per step and rank */
+} hn_ray_sampler;
+int32_t hn_sample_rays(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
+                       float* rays, float* target, void* stream);
+
+/* Training loss (run_nerf.py:612-636 with the data-parallel rule of
+ * SURVEY 8e): loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * (sum sp + sum sp0)
+ * + tv_w * sum tv.  rgb0/sp0/tv may be NULL.  out[4] (device) = loss, mse, mse0,
+ * sum of entropies.  The backward writes the upstream gradients of the five
+ * inputs in torch autograd's op order (mean/pow/div/mul backward), g_loss is
+ * the device scalar d L_total / d loss. */
+int32_t hn_loss_fwd(const float* rgb, const float* rgb0, const float* target, const float* sp,
+                    const float* sp0, int64_t n_rays, const float* tv, int32_t n_tv, float world,
+                    float sparse_w, float tv_w, float* out, void* stream);
+int32_t hn_loss_bwd(const float* rgb, const float* rgb0, const float* target, int64_t n_rays,
+                    int32_t n_tv, float world, float sparse_w, float tv_w, const float* g_loss,
+                    float* g_rgb, float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv, void* stream);
 
 size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
 int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,

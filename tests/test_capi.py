@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(hn):
     for n in names:
         assert hasattr(lib, n), n
         assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
-    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 2
+    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 3
 
 
 def test_struct_sizes_match_header(hn):
@@ -48,6 +48,7 @@ def test_struct_layouts_match_compiled_header(hn, tmp_path):
     structs = {"hn_grid": L.HnGrid, "hn_mlp": L.HnMlp, "hn_mlp_grad": L.HnMlpGrad,
                "hn_render_cfg": L.HnRenderCfg, "hn_render_fwd_args": L.HnRenderFwdArgs,
                "hn_render_bwd_args": L.HnRenderBwdArgs, "hn_tv_args": L.HnTvArgs,
+               "hn_ray_sampler": L.HnRaySampler,
                "hn_radam_tensor": L.HnRadamTensor}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hashnerf_amd.h"', "int main(void) {"]
     for cname, cls in structs.items():
