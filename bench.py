@@ -41,7 +41,7 @@ UNIQUE_PTS = 192               # per ray (the 64 coarse points recur in the fine
 PATH_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2 + 36
 BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2        # bwd kernel: re-gather + scatter-add
 FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
-BWD_KERNELS = ("render_bwd_kernel", "render_scatter_kernel", "slab_reduce_kernel")
+BWD_KERNELS = ("render_bwd_kernel", "slab_reduce_kernel")   # the hn_render_bwd launch
 
 
 def measured_traffic(cfg_id, n_rand_override):
@@ -52,12 +52,13 @@ def measured_traffic(cfg_id, n_rand_override):
     them live; None when no file matches this workload."""
     path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}.json")
     if n_rand_override or not os.path.exists(path):
-        return None, None
+        return None, None, None
     t = json.load(open(path))
     ks = t.get("kernels", {})
     if not all(k in ks for k in BWD_KERNELS):
-        return None, None
-    return sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in BWD_KERNELS), t.get("source")
+        return None, None, None
+    return (sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in BWD_KERNELS), t.get("source"),
+            sum(ks[k].get("atomic_requests", 0.0) for k in BWD_KERNELS) or None)
 
 
 def cpu_baseline(cfg, seconds=12.0, n_rays=256):
@@ -182,7 +183,7 @@ def main():
     B = cfg["N_rand"]
     value = world * B * args.steps / dt
     if rank == 0:
-        traffic, traffic_src = measured_traffic(cfg_id, args.n_rand)
+        traffic, traffic_src, atomics = measured_traffic(cfg_id, args.n_rand)
         bwd_gbs = B * BWD_BYTES_PER_RAY / (bwd_ms * 1e-3) / 1e9
         fwd_gbs = B * FWD_BYTES_PER_RAY / (fwd_ms * 1e-3) / 1e9
         line = {
@@ -200,7 +201,11 @@ def main():
                          "traffic": round(traffic) if traffic else None,
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": B * BWD_BYTES_PER_RAY,
-                         "bytes_per_ray": BWD_BYTES_PER_RAY, "launch_ms": round(bwd_ms, 4)},
+                         "bytes_per_ray": BWD_BYTES_PER_RAY, "launch_ms": round(bwd_ms, 4),
+                         # the binding resource of this launch: memory-side float-atomic
+                         # requests (TCC_EA0_ATOMIC, same PMC passes) per second
+                         "atomic_requests": round(atomics) if atomics else None,
+                         "atomic_Greq_per_s": round(atomics / (bwd_ms * 1e-3) / 1e9, 2) if atomics else None},
             "kernels": {"render_fwd_ms": round(fwd_ms, 4), "render_fwd_GBs": round(fwd_gbs, 1),
                         "render_bwd_ms": round(bwd_ms, 4),
                         "path_GBs": round(value / world * PATH_BYTES_PER_RAY / 1e9, 1),

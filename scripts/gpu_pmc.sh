@@ -48,7 +48,10 @@ traffic = {"bench_args": bench_args, "source": f"pmc_{tag}", "kernels": {}}
 for k, cs in agg.items():
     f, w = cs.get("FETCH_SIZE"), cs.get("WRITE_SIZE")
     if f and w:
-        traffic["kernels"][k.replace("hn::", "")] = {
-            "fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
+        ent = {"fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
+        a = cs.get("TCC_EA0_ATOMIC_sum")
+        if a:
+            ent["atomic_requests"] = sum(a) / len(a)
+        traffic["kernels"][k.replace("hn::", "")] = ent
 json.dump(traffic, open(f"{out}/traffic_{tag}.json", "w"), indent=1)
 EOF
