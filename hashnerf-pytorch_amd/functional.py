@@ -195,6 +195,101 @@ def sample_pdf(bins: torch.Tensor, weights: torch.Tensor, u: torch.Tensor) -> to
 # --------------------------------------------------------------------------
 # fused render_rays (run_nerf_helpers.py:464-574)
 # --------------------------------------------------------------------------
+class RenderState:
+    """Buffers one fused forward leaves for its backward (z values, raw
+    outputs, coarse origin of each fine sample, hash features, the workspace
+    holding the packed weights)."""
+    __slots__ = ("cfg", "rays", "noise_c", "noise_f", "table", "ws", "z_c", "z_f", "raw_c", "raw_f",
+                 "fine_src", "feat", "wsb", "nbytes")
+
+
+def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat):
+    """hn_render_fwd (run_nerf_helpers.py:464-574, forward).  Returns the
+    output dict and a RenderState (None when keep_feat is False)."""
+    L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
+    rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
+                                                                      noise_c, noise_f))
+    ws = [w.contiguous() for w in ws]
+    B = rays.shape[0]
+    dev = rays.device
+    e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)
+    out = dict(rgb=e(B, 3), depth=e(B), acc=e(B), sparsity=e(B), rgb0=e(B, 3), depth0=e(B),
+               acc0=e(B), sparsity0=e(B), z_std=e(B), z_coarse=e(B, 64), z_fine=e(B, 192),
+               raw_c=e(B, 64, 4), raw_f=e(B, 192, 4))
+    a = L.HnRenderFwdArgs()
+    a.n_rays = B
+    for k, t in (("rays", rays), ("t_vals", t_vals), ("t_rand", t_rand), ("u", u),
+                 ("noise_c", noise_c), ("noise_f", noise_f), ("table", table)):
+        setattr(a, k, None if t is None else t.data_ptr())
+    a.coarse = L.make_mlp(ws[:5])
+    a.fine = L.make_mlp(ws[5:])
+    for k, t in out.items():
+        setattr(a, k, t.data_ptr())
+    fine_src = torch.empty((B, 192), dtype=torch.uint8, device=dev)
+    a.fine_src = fine_src.data_ptr()
+    # hash features of every evaluated point, kept for the backward only
+    # when a gradient will be taken (inference skips the 32 KB/ray store)
+    feat = torch.empty((B, L.RENDER_FEAT_PER_RAY) if keep_feat else (0,), dtype=torch.float32,
+                       device=dev)
+    a.feat = feat.data_ptr() if keep_feat else None
+    nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
+    wsb = _ws(nbytes, dev)
+    t0 = TIMER.begin("render_fwd")
+    L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
+    TIMER.end("render_fwd", t0)
+    if DEBUG_KEEP:
+        LAST.update({k: out[k] for k in ("z_coarse", "z_fine", "raw_c", "raw_f")})
+    st = None
+    if keep_feat:
+        st = RenderState()
+        st.cfg, st.rays, st.noise_c, st.noise_f, st.table, st.ws = cfg, rays, noise_c, noise_f, table, ws
+        st.z_c, st.z_f, st.raw_c, st.raw_f = out["z_coarse"], out["z_fine"], out["raw_c"], out["raw_f"]
+        st.fine_src, st.feat, st.wsb, st.nbytes = fine_src, feat, wsb, nbytes
+    return out, st
+
+
+def render_bwd(st: RenderState, grads: dict, d_table, dws):
+    """hn_render_bwd: accumulates (+=) d loss / d table into d_table and the
+    ten NeRFSmall weight gradients into dws (coarse 5, fine 5).  grads: any
+    of g_rgb, g_depth, g_acc, g_sparsity, g_rgb0, g_depth0, g_acc0,
+    g_sparsity0, g_raw_f (missing = 0)."""
+    B = st.rays.shape[0]
+    dev = st.rays.device
+    a = L.HnRenderBwdArgs()
+    a.n_rays = B
+    a.coarse = L.make_mlp(st.ws[:5])
+    a.fine = L.make_mlp(st.ws[5:])
+    keep = []
+    names = ("g_rgb", "g_depth", "g_acc", "g_sparsity", "g_rgb0", "g_depth0", "g_acc0", "g_sparsity0",
+             "g_raw_f")
+    for k, t in [(n, grads.get(n)) for n in names] + [
+            ("rays", st.rays), ("noise_c", st.noise_c), ("noise_f", st.noise_f), ("table", st.table),
+            ("z_coarse", st.z_c), ("z_fine", st.z_f), ("raw_c", st.raw_c), ("raw_f", st.raw_f),
+            ("d_table", d_table)]:
+        t = L.contig(t)
+        keep.append(t)
+        setattr(a, k, None if t is None else t.data_ptr())
+    a.fine_src = st.fine_src.data_ptr()
+    a.feat = st.feat.data_ptr()
+    a.weights_packed = 1               # same workspace and weights as the forward
+    a.d_coarse = L.make_mlp_grad(dws[:5])
+    a.d_fine = L.make_mlp_grad(dws[5:])
+    t0 = TIMER.begin("render_bwd")
+    L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
+    TIMER.end("render_bwd", t0)
+
+
+def zeros_like_all(ts):
+    """Zeroed tensors shaped like ts, views of ONE flat buffer (one fill)."""
+    n = sum(t.numel() for t in ts)
+    flat = torch.zeros(n, dtype=torch.float32, device=ts[0].device)
+    out, off = [], 0
+    for t in ts:
+        out.append(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
+    return out
+
+
 class RenderRaysFn(torch.autograd.Function):
     """Inputs: rays [B,11], t_vals [64], t_rand [B,64]|None, u [B,128],
     noise_c/noise_f |None, table, 5 coarse + 5 fine NeRFSmall weights.
@@ -203,82 +298,25 @@ class RenderRaysFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg: L.HnRenderCfg, keep_feat: bool, rays, t_vals, t_rand, u, noise_c, noise_f,
                 table, *ws):
-        L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
-        rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
-                                                                          noise_c, noise_f))
-        ws = [w.contiguous() for w in ws]
-        B = rays.shape[0]
-        dev = rays.device
-        e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)
-        out = dict(rgb=e(B, 3), depth=e(B), acc=e(B), sparsity=e(B), rgb0=e(B, 3), depth0=e(B),
-                   acc0=e(B), sparsity0=e(B), z_std=e(B), z_coarse=e(B, 64), z_fine=e(B, 192),
-                   raw_c=e(B, 64, 4), raw_f=e(B, 192, 4))
-        a = L.HnRenderFwdArgs()
-        a.n_rays = B
-        for k, t in (("rays", rays), ("t_vals", t_vals), ("t_rand", t_rand), ("u", u),
-                     ("noise_c", noise_c), ("noise_f", noise_f), ("table", table)):
-            setattr(a, k, None if t is None else t.data_ptr())
-        a.coarse = L.make_mlp(ws[:5])
-        a.fine = L.make_mlp(ws[5:])
-        for k, t in out.items():
-            setattr(a, k, t.data_ptr())
-        fine_src = torch.empty((B, 192), dtype=torch.uint8, device=dev)
-        a.fine_src = fine_src.data_ptr()
-        # hash features of every evaluated point, kept for the backward only
-        # when a gradient will be taken (inference skips the 32 KB/ray store)
-        feat = torch.empty((B, L.RENDER_FEAT_PER_RAY) if keep_feat else (0,), dtype=torch.float32,
-                           device=dev)
-        a.feat = feat.data_ptr() if keep_feat else None
-        nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
-        wsb = _ws(nbytes, dev)
-        t0 = TIMER.begin("render_fwd")
-        L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
-        TIMER.end("render_fwd", t0)
-        if DEBUG_KEEP:
-            LAST.update({k: out[k] for k in ("z_coarse", "z_fine", "raw_c", "raw_f")})
-        ctx.cfg = cfg
-        ctx.wsb = wsb                      # holds the packed weights for the backward
+        out, st = render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat)
+        ctx.st = st
         ctx.set_materialize_grads(False)   # unused outputs => NULL, not zeros (0*inf)
-        ctx.has_noise = (noise_c is not None, noise_f is not None)
-        ctx.save_for_backward(rays, noise_c if noise_c is not None else rays,
-                              noise_f if noise_f is not None else rays, table, out["z_coarse"],
-                              out["z_fine"], out["raw_c"], out["raw_f"], fine_src, feat, *ws)
         ctx.mark_non_differentiable(out["z_std"])
         return (out["rgb"], out["depth"], out["acc"], out["sparsity"], out["rgb0"], out["depth0"],
                 out["acc0"], out["sparsity0"], out["z_std"], out["raw_f"])
 
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_acc, g_sp, g_rgb0, g_depth0, g_acc0, g_sp0, _g_zstd, g_raw):
-        rays, noise_c, noise_f, table, z_c, z_f, raw_c, raw_f, fine_src, feat, *ws = ctx.saved_tensors
-        noise_c = noise_c if ctx.has_noise[0] else None
-        noise_f = noise_f if ctx.has_noise[1] else None
-        B = rays.shape[0]
-        dev = rays.device
-        d_table = torch.zeros_like(table)
-        dws = [torch.zeros_like(w) for w in ws]
-        a = L.HnRenderBwdArgs()
-        a.n_rays = B
-        a.coarse = L.make_mlp(ws[:5])
-        a.fine = L.make_mlp(ws[5:])
-        grads = dict(g_rgb=g_rgb, g_depth=g_depth, g_acc=g_acc, g_sparsity=g_sp, g_rgb0=g_rgb0,
-                     g_depth0=g_depth0, g_acc0=g_acc0, g_sparsity0=g_sp0, g_raw_f=g_raw)
-        keep = []
-        for k, t in list(grads.items()) + [("rays", rays), ("noise_c", noise_c), ("noise_f", noise_f),
-                                           ("table", table), ("z_coarse", z_c), ("z_fine", z_f),
-                                           ("raw_c", raw_c), ("raw_f", raw_f), ("d_table", d_table)]:
-            t = L.contig(t)
-            keep.append(t)
-            setattr(a, k, None if t is None else t.data_ptr())
-        a.fine_src = fine_src.data_ptr()
-        a.feat = feat.data_ptr()
-        a.weights_packed = 1               # same workspace and weights as the forward
-        a.d_coarse = L.make_mlp_grad(dws[:5])
-        a.d_fine = L.make_mlp_grad(dws[5:])
-        nbytes = L.lib().hn_render_workspace_bytes(ctx.cfg, B)
-        wsb = ctx.wsb
-        t0 = TIMER.begin("render_bwd")
-        L.check(L.lib().hn_render_bwd(ctx.cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_bwd")
-        TIMER.end("render_bwd", t0)
+        st = ctx.st
+        if st is None:
+            raise RuntimeError("hashnerf_amd.render_rays: forward ran without keeping features "
+                               "(no input required grad)")
+        d_table = torch.zeros_like(st.table)
+        dws = zeros_like_all(st.ws)
+        render_bwd(st, dict(g_rgb=g_rgb, g_depth=g_depth, g_acc=g_acc, g_sparsity=g_sp, g_rgb0=g_rgb0,
+                            g_depth0=g_depth0, g_acc0=g_acc0, g_sparsity0=g_sp0, g_raw_f=g_raw),
+                   d_table, dws)
+        ctx.st = None
         return (None, None, None, None, None, None, None, None, d_table, *dws)
 
 
@@ -307,6 +345,34 @@ def sample_rays(image, c2w, n_rays, K, near, far, crop, seed):
     return rays, target
 
 
+def loss_fwd(rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w):
+    """hn_loss_fwd -> device [4] = loss, mse, mse0, sum of entropies."""
+    L.require_device(rgb, target, sp)
+    n = rgb.shape[0]
+    out = torch.empty(4, dtype=torch.float32, device=rgb.device)
+    L.check(L.lib().hn_loss_fwd(L.ptr(L.contig(rgb)), L.ptr(L.contig(rgb0)), L.ptr(L.contig(target)),
+                                L.ptr(L.contig(sp)), L.ptr(L.contig(sp0)), n, L.ptr(L.contig(tv)),
+                                0 if tv is None else tv.numel(), float(world), float(sparse_w),
+                                float(tv_w), L.ptr(out), L.stream(rgb.device)), "loss_fwd")
+    return out
+
+
+def loss_bwd(rgb, rgb0, target, n_tv, world, sparse_w, tv_w, g_loss, has_sp0=True):
+    """hn_loss_bwd -> (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) for upstream g_loss (device scalar)."""
+    n = rgb.shape[0]
+    dev = rgb.device
+    g_rgb = torch.empty_like(rgb)
+    g_rgb0 = torch.empty_like(rgb) if rgb0 is not None else None
+    g_sp = torch.empty(n, dtype=torch.float32, device=dev)
+    g_sp0 = torch.empty(n, dtype=torch.float32, device=dev) if has_sp0 else None
+    g_tv = torch.empty(n_tv, dtype=torch.float32, device=dev) if n_tv else None
+    L.check(L.lib().hn_loss_bwd(L.ptr(L.contig(rgb)), L.ptr(L.contig(rgb0)), L.ptr(L.contig(target)), n,
+                                n_tv, float(world), float(sparse_w), float(tv_w), L.ptr(g_loss.contiguous()),
+                                L.ptr(g_rgb), L.ptr(g_rgb0), L.ptr(g_sp), L.ptr(g_sp0), L.ptr(g_tv),
+                                L.stream(dev)), "loss_bwd")
+    return g_rgb, g_rgb0, g_sp, g_sp0, g_tv
+
+
 class TrainLossFn(torch.autograd.Function):
     """loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * (sum sp + sum sp0) +
     tv_w * sum tv (run_nerf.py:612-636 under train.dp_loss's DP rule).
@@ -314,19 +380,9 @@ class TrainLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w):
-        L.require_device(rgb, target, sp)
-        rgb, target, sp = rgb.contiguous(), target.contiguous(), sp.contiguous()
-        rgb0 = None if rgb0 is None else rgb0.contiguous()
-        sp0 = None if sp0 is None else sp0.contiguous()
-        tv = None if tv is None else tv.contiguous()
-        n = rgb.shape[0]
-        out = torch.empty(4, dtype=torch.float32, device=rgb.device)
-        L.check(L.lib().hn_loss_fwd(L.ptr(rgb), L.ptr(rgb0), L.ptr(target), L.ptr(sp), L.ptr(sp0), n,
-                                    L.ptr(tv), 0 if tv is None else tv.numel(), float(world),
-                                    float(sparse_w), float(tv_w), L.ptr(out), L.stream(rgb.device)),
-                "loss_fwd")
+        out = loss_fwd(rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w)
         ctx.save_for_backward(rgb, rgb0 if rgb0 is not None else rgb, target)
-        ctx.has = (rgb0 is not None, sp0 is not None, tv is not None)
+        ctx.has = (rgb0 is not None, sp0 is not None)
         ctx.n_tv = 0 if tv is None else tv.numel()
         ctx.consts = (float(world), float(sparse_w), float(tv_w))
         mse, mse0 = out[1], out[2]
@@ -336,20 +392,10 @@ class TrainLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, _g_mse, _g_mse0):
         rgb, rgb0, target = ctx.saved_tensors
-        has0, has_sp0, has_tv = ctx.has
-        rgb0 = rgb0 if has0 else None
-        n = rgb.shape[0]
-        dev = rgb.device
-        g = (g_loss if g_loss is not None else torch.ones((), device=dev)).contiguous()
-        g_rgb = torch.empty_like(rgb)
-        g_rgb0 = torch.empty_like(rgb) if has0 else None
-        g_sp = torch.empty(n, dtype=torch.float32, device=dev)
-        g_sp0 = torch.empty(n, dtype=torch.float32, device=dev) if has_sp0 else None
-        g_tv = torch.empty(ctx.n_tv, dtype=torch.float32, device=dev) if has_tv else None
-        world, sparse_w, tv_w = ctx.consts
-        L.check(L.lib().hn_loss_bwd(L.ptr(rgb), L.ptr(rgb0), L.ptr(target), n, ctx.n_tv, world, sparse_w,
-                                    tv_w, L.ptr(g), L.ptr(g_rgb), L.ptr(g_rgb0), L.ptr(g_sp),
-                                    L.ptr(g_sp0), L.ptr(g_tv), L.stream(dev)), "loss_bwd")
+        has0, has_sp0 = ctx.has
+        g = g_loss if g_loss is not None else torch.ones((), device=rgb.device)
+        g_rgb, g_rgb0, g_sp, g_sp0, g_tv = loss_bwd(rgb, rgb0 if has0 else None, target, ctx.n_tv,
+                                                    *ctx.consts, g, has_sp0)
         return g_rgb, g_rgb0, None, g_sp, g_sp0, g_tv, None, None, None
 
 
@@ -357,26 +403,44 @@ def train_loss(rgb, rgb0, target, sp, sp0, tv=None, world=1, sparse_w=0.0, tv_w=
     return TrainLossFn.apply(rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w)
 
 
+def _tv_args(table, mv, cubes, log2T):
+    a = L.HnTvArgs()
+    a.n_levels = table.shape[0]
+    a.log2_hashmap_size = int(log2T)
+    for l, c in enumerate(cubes):
+        a.cube[l] = int(c)
+    a.min_vertex = mv.data_ptr()
+    a.table = table.data_ptr()
+    return a
+
+
+def tv_fwd(table, min_vertex, cubes, log2T):
+    """hn_tv_fwd: per-level TV values [L]; returns (tv, device min vertices)."""
+    L.require_device(table)
+    mv = min_vertex.to(dtype=torch.int32).contiguous()
+    if mv.device.type == "cpu":            # no host stall: pinned + async copy
+        mv = mv.pin_memory().to(table.device, non_blocking=True)
+    else:
+        mv = mv.to(table.device)
+    tv = torch.empty(table.shape[0], dtype=torch.float32, device=table.device)
+    L.check(L.lib().hn_tv_fwd(_tv_args(table, mv, cubes, log2T), L.ptr(tv), L.stream(table.device)),
+            "tv_fwd")
+    return tv, mv
+
+
+def tv_bwd(table, mv, cubes, log2T, g_tv, dtable):
+    """hn_tv_bwd: dtable += sum_l g_tv[l] d tv_l / d table."""
+    g = g_tv.contiguous()
+    L.check(L.lib().hn_tv_bwd(_tv_args(table, mv, cubes, log2T), L.ptr(g), L.ptr(dtable),
+                              L.stream(table.device)), "tv_bwd")
+
+
 class TVFn(torch.autograd.Function):
     """Per-level hash-table TV (loss.py:11-43) for all levels in one launch."""
 
     @staticmethod
     def forward(ctx, table, min_vertex, cubes, log2T):
-        L.require_device(table)
-        a = L.HnTvArgs()
-        a.n_levels = table.shape[0]
-        a.log2_hashmap_size = int(log2T)
-        for l, c in enumerate(cubes):
-            a.cube[l] = int(c)
-        mv = min_vertex.to(dtype=torch.int32).contiguous()
-        if mv.device.type == "cpu":            # no host stall: pinned + async copy
-            mv = mv.pin_memory().to(table.device, non_blocking=True)
-        else:
-            mv = mv.to(table.device)
-        a.min_vertex = mv.data_ptr()
-        a.table = table.data_ptr()
-        tv = torch.empty(table.shape[0], dtype=torch.float32, device=table.device)
-        L.check(L.lib().hn_tv_fwd(a, L.ptr(tv), L.stream(table.device)), "tv_fwd")
+        tv, mv = tv_fwd(table, min_vertex, cubes, log2T)
         ctx.save_for_backward(table, mv)
         ctx.cubes, ctx.log2T = list(cubes), int(log2T)
         return tv
@@ -384,16 +448,8 @@ class TVFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_tv):
         table, mv = ctx.saved_tensors
-        a = L.HnTvArgs()
-        a.n_levels = table.shape[0]
-        a.log2_hashmap_size = ctx.log2T
-        for l, c in enumerate(ctx.cubes):
-            a.cube[l] = int(c)
-        a.min_vertex = mv.data_ptr()
-        a.table = table.data_ptr()
         dtable = torch.zeros_like(table)
-        g = g_tv.contiguous()
-        L.check(L.lib().hn_tv_bwd(a, L.ptr(g), L.ptr(dtable), L.stream(table.device)), "tv_bwd")
+        tv_bwd(table, mv, ctx.cubes, ctx.log2T, g_tv, dtable)
         return dtable, None, None, None
 
 

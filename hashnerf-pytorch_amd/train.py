@@ -24,7 +24,7 @@ import torch.distributed as dist
 
 from . import functional as HF
 from .create import create_nerf
-from .loss import tv_loss_levels
+from .loss import draw_tv_cubes, tv_loss_levels
 from .rays import bbox_for_blender, blender_cameras, blender_intrinsics
 from .render import img2mse, mse2psnr, render, render_ray_batch
 
@@ -101,15 +101,25 @@ def _step_seed(seed, rank, step):
 
 
 class Trainer:
-    """fused=True (default): device ray sampler (hn_sample_rays) + fused loss
-    (hn_loss_fwd/bwd) around the fused renderer -- a handful of launches per
-    step.  fused=False: the same step in eager torch ops (randperm sampling,
-    img2mse, sums), kept as the op-for-op rendition of run_nerf.py."""
+    """One training iteration of run_nerf.py:541-651.
 
-    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0, fused=True):
+    mode="explicit" (default): the step as an explicit launch sequence -- device
+    ray sampler, fused render forward, TV forward, fused loss forward and
+    backward, render backward and TV backward accumulating into ONE persistent
+    table-gradient buffer, all-reduce, RAdam -- with no autograd graph (the
+    gradients are those autograd computes for the same loss: the loss
+    backward reproduces autograd's op order, the render/TV backwards are the
+    Functions' own backwards).  mode="autograd": the same kernels through the
+    autograd module API (render_rays, TrainLossFn, TVFn).  mode="eager": the
+    module API with eager torch sampling and loss ops (randperm, img2mse,
+    sums), the op-for-op rendition of run_nerf.py."""
+
+    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0, mode="explicit"):
         self.args, self.data, self.device = args, data, torch.device(device)
         self.rank, self.world = rank, world
-        self.seed, self.fused = seed, fused
+        if mode not in ("explicit", "autograd", "eager"):
+            raise ValueError(f"Trainer mode {mode!r}")
+        self.seed, self.mode = seed, mode
         args.bounding_box = data.bounding_box
         torch.manual_seed(seed)                      # identical init on every rank
         (self.kw_train, self.kw_test, self.start, self.grad_vars,
@@ -129,6 +139,7 @@ class Trainer:
                                 torch.arange(W // 2 - dW, W // 2 + dW, device=self.device), indexing="ij")
         self.coords_crop = torch.stack([cj, ci], -1).reshape(-1, 2)
         self.crop = (H // 2 - dH, W // 2 - dW, 2 * dH, 2 * dW)
+        self._grads = None
 
     def sample_rays(self, i: int):
         """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
@@ -161,29 +172,85 @@ class Trainer:
         if self.world > 1:
             allreduce_grads(self.embed_fn.table, self.grad_vars)
 
+    def _fused_setup(self):
+        from .render import _fusable, _linspace_cached
+        kw = self.kw_train
+        nq, nf, nfine = kw["network_query_fn"], kw["network_fn"], kw["network_fine"]
+        if not _fusable(torch.empty(1, 11), nf, nq, kw["N_samples"], kw["N_importance"], nfine):
+            raise NotImplementedError("Trainer(mode='explicit') needs the HashNeRF configuration")
+        a = self.args
+        self._cfg = HF.make_render_cfg(self.embed_fn.grid(), bool(kw.get("white_bkgd", False)),
+                                       bool(kw.get("lindisp", False)), kw.get("perturb", 0.) > 0.)
+        self._t_vals = _linspace_cached(kw["N_samples"], self.device)
+        self._ws = nf.weights() + nfine.weights()
+        table = self.embed_fn.table
+        self._gtable = torch.zeros_like(table)
+        self._gws = HF.zeros_like_all(self._ws)
+        self._one = torch.ones((), device=self.device)
+        self._grads = True
+
+    def _fused_forward_backward(self, i: int):
+        a, d, kw = self.args, self.data, self.kw_train
+        if self._grads is None:
+            self._fused_setup()
+        B = a.N_rand
+        img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
+        crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
+        rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], B, d.K, 2., 6., crop,
+                                      _step_seed(self.seed, self.rank, i))
+        perturb = kw.get("perturb", 0.) > 0.
+        t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
+        u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
+             torch.linspace(0., 1., kw["N_importance"], device=self.device).expand(B, kw["N_importance"]))
+        table = self.embed_fn.table
+        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
+        tv = mv = cubes = None
+        if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
+            cubes, mv0 = draw_tv_cubes(self.embed_fn.n_levels, self.embed_fn.base_resolution,
+                                       self.embed_fn.finest_resolution, self.cpu_gen)
+            tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
+        consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
+        lo = HF.loss_fwd(out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts)
+        g_rgb, g_rgb0, g_sp, g_sp0, g_tv = HF.loss_bwd(out["rgb"], out["rgb0"], target,
+                                                       0 if tv is None else tv.numel(), *consts, self._one)
+        self._gtable.zero_()
+        self._gws[0]._base.zero_()                      # the ten MLP grads share one flat buffer
+        HF.render_bwd(st, dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0),
+                      self._gtable, self._gws)
+        if tv is not None:
+            HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
+        table.grad = self._gtable
+        for p, g in zip(self._ws, self._gws):
+            p.grad = g
+        return lo[0], lo[1]
+
     def step(self, i: int):
         a = self.args
-        self.optimizer.zero_grad(set_to_none=True)
-        if self.fused:
-            d = self.data
-            img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
-            crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
-            rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
-                                          _step_seed(self.seed, self.rank, i))
-            rgb, depth, acc, extras = render_ray_batch(rays, (a.N_rand,), chunk=a.chunk, retraw=True,
-                                                       **self.kw_train)
-            tv = None
-            if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
-                tv = tv_loss_levels(self.embed_fn, generator=self.cpu_gen)
-            loss, mse, _ = HF.train_loss(rgb, extras.get("rgb0"), target, extras["sparsity_loss"],
-                                         extras.get("sparsity_loss0"), tv, self.world, a.sparse_loss_weight,
-                                         a.tv_loss_weight)
+        if self.mode == "explicit":
+            loss, mse = self._fused_forward_backward(i)
         else:
-            batch_rays, target = self.sample_rays(i)
-            rgb, depth, acc, extras = render(self.data.H, self.data.W, self.data.K, chunk=a.chunk,
-                                             rays=batch_rays, retraw=True, near=2., far=6., **self.kw_train)
-            loss, mse = self.loss_fn(rgb, extras, target, i)
-        loss.backward()
+            self.optimizer.zero_grad(set_to_none=True)
+            if self.mode == "autograd":
+                d = self.data
+                img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
+                crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
+                rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
+                                              _step_seed(self.seed, self.rank, i))
+                rgb, depth, acc, extras = render_ray_batch(rays, (a.N_rand,), chunk=a.chunk, retraw=True,
+                                                           **self.kw_train)
+                tv = None
+                if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
+                    tv = tv_loss_levels(self.embed_fn, generator=self.cpu_gen)
+                loss, mse, _ = HF.train_loss(rgb, extras.get("rgb0"), target, extras["sparsity_loss"],
+                                             extras.get("sparsity_loss0"), tv, self.world,
+                                             a.sparse_loss_weight, a.tv_loss_weight)
+            else:
+                batch_rays, target = self.sample_rays(i)
+                rgb, depth, acc, extras = render(self.data.H, self.data.W, self.data.K, chunk=a.chunk,
+                                                 rays=batch_rays, retraw=True, near=2., far=6.,
+                                                 **self.kw_train)
+                loss, mse = self.loss_fn(rgb, extras, target, i)
+            loss.backward()
         self.allreduce_grads()
         self.optimizer.step()
         decay_steps = a.lrate_decay * 1000
