@@ -12,4 +12,4 @@ build.build_variant(["-DHN_PROFILE=1"], "/tmp/hn_profile.so")
 PY
 HN_LIB_PATH=/tmp/hn_profile.so timeout -k 10 300 python bench.py --steps 4 --warmup 2 --no-cpu-baseline "$@" \
     > $OUT/b1_profile.json 2> $OUT/b1_profile.err || exit 1
-grep hn_b1_profile $OUT/b1_profile.err | tail -4
+grep 'hn_b1_' $OUT/b1_profile.err | tail -6
