@@ -35,15 +35,18 @@ def get_rays_np(H, W, K, c2w):
 
 
 def get_ndc_rays(H, W, focal, near, rays_o, rays_d):
-    """ray_util.py:96-142 (forward-facing scenes)."""
+    """ray_util.py:96-142 (forward-facing scenes), in the reference's op order
+    (ox/oz and oy/oz formed once; d2 = 1 - o2)."""
     t = -(near + rays_o[..., 2]) / rays_d[..., 2]
     rays_o = rays_o + t[..., None] * rays_d
-    o0 = -1. / (W / (2. * focal)) * rays_o[..., 0] / rays_o[..., 2]
-    o1 = -1. / (H / (2. * focal)) * rays_o[..., 1] / rays_o[..., 2]
+    ox_oz = rays_o[..., 0] / rays_o[..., 2]
+    oy_oz = rays_o[..., 1] / rays_o[..., 2]
+    o0 = -1. / (W / (2. * focal)) * ox_oz
+    o1 = -1. / (H / (2. * focal)) * oy_oz
     o2 = 1. + 2. * near / rays_o[..., 2]
-    d0 = -1. / (W / (2. * focal)) * (rays_d[..., 0] / rays_d[..., 2] - rays_o[..., 0] / rays_o[..., 2])
-    d1 = -1. / (H / (2. * focal)) * (rays_d[..., 1] / rays_d[..., 2] - rays_o[..., 1] / rays_o[..., 2])
-    d2 = -2. * near / rays_o[..., 2]
+    d0 = -1. / (W / (2. * focal)) * (rays_d[..., 0] / rays_d[..., 2] - ox_oz)
+    d1 = -1. / (H / (2. * focal)) * (rays_d[..., 1] / rays_d[..., 2] - oy_oz)
+    d2 = 1 - o2
     return torch.stack([o0, o1, o2], -1), torch.stack([d0, d1, d2], -1)
 
 

@@ -249,8 +249,12 @@ def render_ray_batch(rays_, out_shape, chunk=1024 * 32, **kwargs):
 @torch.no_grad()
 def render_path(render_poses, hwf, K, chunk, render_kwargs, gt_imgs=None, savedir=None,
                 render_factor=0):
-    """run_nerf_helpers.py:395-459 (evaluation; returns rgbs, depths and,
-    when gt_imgs is given, the per-image PSNRs)."""
+    """run_nerf_helpers.py:395-459 (evaluation): returns (rgbs, depths), depth
+    normalised to [0, 1] between near and far.  With gt_imgs (and no
+    render_factor) the per-image PSNRs are computed as the reference does and,
+    when savedir is given, pickled to test_psnrs_avg{avg:0.2f}.pkl like
+    :452-456.  The per-frame matplotlib figures (:435-449) are not written:
+    plotting is outside the hot path."""
     H, W, focal = hwf
     near, far = render_kwargs["near"], render_kwargs["far"]
     if render_factor != 0:
@@ -263,4 +267,11 @@ def render_path(render_poses, hwf, K, chunk, render_kwargs, gt_imgs=None, savedi
         if gt_imgs is not None and render_factor == 0:
             gt = gt_imgs[i].cpu().numpy() if torch.is_tensor(gt_imgs[i]) else gt_imgs[i]
             psnrs.append(-10. * np.log10(np.mean(np.square(rgbs[-1] - gt))))
-    return np.stack(rgbs, 0), np.stack(depths, 0), psnrs
+    if gt_imgs is not None and render_factor == 0 and savedir is not None and psnrs:
+        import os
+        import pickle
+        avg = sum(psnrs) / len(psnrs)
+        with open(os.path.join(savedir, "test_psnrs_avg{:0.2f}.pkl".format(avg)), "wb") as fp:
+            pickle.dump(psnrs, fp)
+    render_path.last_psnrs = psnrs
+    return np.stack(rgbs, 0), np.stack(depths, 0)

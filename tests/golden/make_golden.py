@@ -291,6 +291,44 @@ def gen_render(ref, name, T=14, finest=512, B=64, white=True, perturb=1.0, seed=
     save(name, **arrays)
 
 
+def gen_ndc(ref):
+    """ray_util.get_ndc_rays on LLFF-like forward-facing rays (run_nerf_helpers.py:349)."""
+    H, W, focal = 30, 40, 35.0
+    g = rng(31)
+    ro = torch.from_numpy(g.normal(0, 0.3, (200, 3)).astype(np.float32))
+    ro[:, 2] += 0.5
+    rd = torch.from_numpy(g.normal(0, 0.2, (200, 3)).astype(np.float32))
+    rd[:, 2] = -1.0 + rd[:, 2] * 0.1
+    o, d = ref.ray_util.get_ndc_rays(H, W, focal, 1.0, ro, rd)
+    save("ndc", H=H, W=W, focal=focal, near=1.0, rays_o=ro.numpy(), rays_d=rd.numpy(),
+         ndc_o=o.numpy(), ndc_d=d.numpy())
+
+
+def gen_render_image(ref, T=12, finest=256, H=12, W=14, seed=23):
+    """render() over a whole image from c2w (run_nerf_helpers.py:310-392, the
+    render_path inner call, :418) with a chunk smaller than the image, det
+    sampling (pytest hooks), white background."""
+    cams, box, K, focal = scene(ref, H, W)
+    emb, tab = make_embedder(ref, box, T, finest, seed)
+    shenc = ref.sh.SHEncoder()
+    mc, mf = make_mlps(ref, seed)
+    nq = lambda inputs, viewdirs, fn: ref.rnh.run_network(inputs, viewdirs, fn, embed_fn=emb,
+                                                          embeddirs_fn=shenc, netchunk=65536)
+    kw = dict(network_query_fn=nq, perturb=0., N_importance=128, network_fine=mf,
+              N_samples=64, network_fn=mc, embed_fn=emb, use_viewdirs=True, white_bkgd=True,
+              raw_noise_std=0., ndc=False, lindisp=False, near=2., far=6., pytest=True)
+    pose = cams[7][:3, :4]
+    with torch.no_grad():
+        rgb, depth, acc, extras = ref.rnh.render(H, W, K, chunk=50, c2w=pose, **kw)
+    arrays = dict(box_min=box[0].numpy(), box_max=box[1].numpy(), log2T=T, finest=finest,
+                  table_seed=seed, H=H, W=W, K=K, c2w=pose.numpy(), rgb=rgb.numpy(),
+                  depth=depth.numpy(), acc=acc.numpy(), rgb0=extras["rgb0"].numpy())
+    for tag, m in (("c", mc), ("f", mf)):
+        for k, v in m.named_parameters():
+            arrays[f"w{tag}:{k}"] = v.detach().numpy()
+    save("render_image", **arrays)
+
+
 def gen_tv(ref):
     T = 12
     box = (torch.tensor([-1., -1., -1.]), torch.tensor([1., 1., 1.]))
@@ -347,6 +385,10 @@ def gen_radam(ref):
 def main():
     torch.set_num_threads(8)
     ref = load_reference()
+    if len(sys.argv) > 1:            # regenerate selected fixtures only, e.g. `ndc render_image`
+        for name in sys.argv[1:]:
+            globals()["gen_" + name](ref)
+        return
     gen_hash(ref)
     gen_encode(ref)
     gen_sh(ref)
@@ -358,6 +400,8 @@ def main():
     gen_radam(ref)
     gen_render(ref, "render_white_perturb", white=True, perturb=1.0, seed=21)
     gen_render(ref, "render_black_det", white=False, perturb=0.0, seed=22, T=13, finest=1024)
+    gen_ndc(ref)
+    gen_render_image(ref)
 
 
 if __name__ == "__main__":

@@ -287,3 +287,30 @@ def test_radam_trace_vs_reference(hn):
         np.testing.assert_array_equal(pa.detach().cpu().numpy(), g["pa"][step], f"pa step {step}")
         np.testing.assert_array_equal(pb.detach().cpu().numpy(), g["pb"][step], f"pb step {step}")
     assert opt.state[pa]["step"] == 8
+
+
+def test_render_image_from_c2w_vs_reference(hn):
+    """render(H, W, K, c2w=...) over a whole image with a chunk smaller than
+    the image (run_nerf_helpers.py:310-392, the render_path inner call),
+    inference (no grad: features not kept), det sampling, against the
+    reference's render on the same scene."""
+    g = golden("render_image")
+    emb, mc, mf = _scene_from_golden(hn, g)
+    H, W = int(g["H"]), int(g["W"])
+    kw = dict(network_query_fn=hn.NetworkQuery(emb, hn.SHEncoder()), perturb=0., N_importance=128,
+              network_fine=mf, N_samples=64, network_fn=mc, embed_fn=emb, use_viewdirs=True,
+              white_bkgd=True, raw_noise_std=0., ndc=False, lindisp=False, near=2., far=6., pytest=True)
+    with torch.no_grad():
+        rgb, depth, acc, extras = hn.render(H, W, g["K"], chunk=50, c2w=g2t(g["c2w"]), **kw)
+    assert rgb.shape == (H, W, 3) and depth.shape == (H, W)
+    close(extras["rgb0"].reshape(-1, 3), g["rgb0"].reshape(-1, 3), rtol=1e-4, atol=1e-5, msg="rgb0")
+    mostly_close(rgb.reshape(-1, 3), g["rgb"].reshape(-1, 3), rtol=1e-4, atol=1e-5, frac=0.6, loose=2e-2,
+                 msg="rgb")
+    mostly_close(acc.reshape(-1), g["acc"].reshape(-1), rtol=1e-4, atol=1e-5, frac=0.6, loose=2e-2,
+                 msg="acc")
+    # render_path: same frames, normalised depth, reference return signature
+    kw_path = dict(kw)
+    rgbs, depths = hn.render_path(torch.stack([g2t(g["c2w"])] * 2), (H, W, None), g["K"], 50, kw_path)
+    assert rgbs.shape == (2, H, W, 3) and depths.shape == (2, H, W)
+    np.testing.assert_allclose(rgbs[0], rgb.cpu().numpy(), rtol=0, atol=0)
+    np.testing.assert_allclose(depths[1], ((depth - 2.) / 4.).cpu().numpy(), rtol=1e-6, atol=1e-7)

@@ -146,3 +146,12 @@ def test_render_rays_step(oracle, name):
     for tag, w in (("c", wc), ("f", wf)):
         for k in oracle.MLP_KEYS:
             np.testing.assert_allclose(w[k].grad.numpy(), g[f"g{tag}:{k}"], rtol=1e-4, atol=1e-7)
+
+
+def test_ndc_rays_bitexact_vs_reference(hn):
+    """rays.get_ndc_rays against ray_util.get_ndc_rays (golden, same op order)."""
+    g = golden("ndc")
+    o, d = hn.get_ndc_rays(int(g["H"]), int(g["W"]), float(g["focal"]), float(g["near"]),
+                           torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"]))
+    np.testing.assert_array_equal(o.numpy(), g["ndc_o"])
+    np.testing.assert_array_equal(d.numpy(), g["ndc_d"])
