@@ -36,7 +36,11 @@ __global__ __launch_bounds__(256) void tv_fwd_kernel(TvK k, float* __restrict__ 
   const int t = blockIdx.x * 256 + threadIdx.x;
   float acc = 0.f;
   if (t < n1 * n1 * n1) {
-    const int i = t / (n1 * n1), j = (t / n1) % n1, kk = t % n1;   // meshgrid 'ij' order
+    // x fastest across the lanes: h(x..x+7) of one (y, z) fill one 64-B
+    // segment, so neighbouring lanes' gathers share cache lines (the TV sum is
+    // order-free up to fp32 rounding; the reference's 'ij' order is only its
+    // summation order)
+    const int i = t % n1, j = (t / n1) % n1, kk = t / (n1 * n1);
     const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
                    z = (uint32_t)(k.mv[3 * l + 2] + kk);
     const float2 e = tv_row(k, l, x, y, z);
@@ -48,37 +52,37 @@ __global__ __launch_bounds__(256) void tv_fwd_kernel(TvK k, float* __restrict__ 
   if (threadIdx.x == 0 && s != 0.f) atomic_add_f32(tv + l, s / (float)c);
 }
 
+// One thread per (vertex, feature), x fastest: the two features of a row
+// are adjacent lanes and 8 consecutive x of one (y, z) share a 64-B segment,
+// so one wave-instruction of atomics is ~8 memory requests instead of 64.
+HN_DEV float tv_val(const TvK& k, int l, uint32_t x, uint32_t y, uint32_t z, int f) {
+  const uint32_t mask = (1u << k.log2T) - 1u;
+  const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
+  return k.table[((((size_t)l << k.log2T) + h) << 1) + f];
+}
+
 __global__ __launch_bounds__(256) void tv_bwd_kernel(TvK k, const float* __restrict__ g_tv,
                                                      float* __restrict__ dtable) {
   const int l = blockIdx.y;
   const int c = k.cube[l], n1 = c + 1;
   const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= n1 * n1 * n1) return;
-  const int i = t / (n1 * n1), j = (t / n1) % n1, kk = t % n1;
+  const int v = t >> 1, f = t & 1;
+  if (v >= n1 * n1 * n1) return;
+  const int i = v % n1, j = (v / n1) % n1, kk = v / (n1 * n1);
   const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
                  z = (uint32_t)(k.mv[3 * l + 2] + kk);
-  const float2 e = tv_row(k, l, x, y, z);
-  float g0 = 0.f, g1 = 0.f;   // sum over incident edges of d(d^2)/de = -+2d
+  const float e = tv_val(k, l, x, y, z, f);
+  float g = 0.f;   // sum over incident edges of d(d^2)/de = -+2d
   const int idx[3] = {i, j, kk};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    if (idx[a] < c) {
-      const float2 n = tv_row(k, l, x + (a == 0), y + (a == 1), z + (a == 2));
-      g0 -= 2.f * (n.x - e.x);
-      g1 -= 2.f * (n.y - e.y);
-    }
-    if (idx[a] > 0) {
-      const float2 pv = tv_row(k, l, x - (a == 0), y - (a == 1), z - (a == 2));
-      g0 += 2.f * (e.x - pv.x);
-      g1 += 2.f * (e.y - pv.y);
-    }
+    if (idx[a] < c) g -= 2.f * (tv_val(k, l, x + (a == 0), y + (a == 1), z + (a == 2), f) - e);
+    if (idx[a] > 0) g += 2.f * (e - tv_val(k, l, x - (a == 0), y - (a == 1), z - (a == 2), f));
   }
   const float scale = g_tv[l] / (float)c;
   const uint32_t mask = (1u << k.log2T) - 1u;
   const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
-  float* dst = dtable + ((((size_t)l << k.log2T) + h) << 1);
-  atomic_add_f32(dst, scale * g0);
-  atomic_add_f32(dst + 1, scale * g1);
+  atomic_add_f32(dtable + ((((size_t)l << k.log2T) + h) << 1) + f, scale * g);
 }
 
 struct RadamK {
@@ -172,7 +176,7 @@ extern "C" int32_t hn_tv_bwd(const hn_tv_args* a, const float* g_tv, float* dtab
   int32_t st = make_tv(a, k, nb);
   if (st) return st;
   if (!g_tv || !dtable) return HN_E_NULL;
-  hipLaunchKernelGGL(tv_bwd_kernel, dim3(nb, a->n_levels), dim3(256), 0, (hipStream_t)stream, k, g_tv,
+  hipLaunchKernelGGL(tv_bwd_kernel, dim3(2 * nb, a->n_levels), dim3(256), 0, (hipStream_t)stream, k, g_tv,
                      dtable);
   return hip_status(hipGetLastError());
 }

@@ -157,7 +157,13 @@ HN_DEV void stage_grid_sizes(const GridArgs& g, float* gsl) {
 constexpr int kFZc = 0, kFZsrc = 64, kFZs = 256, kFRaw = 448, kFW = 1216, kFBins = 1280,
               kFCdf = 1344, kFLds = 1408;
 
-__global__ __launch_bounds__(256) void render_fwd_kernel(RenderK k) {
+#ifndef HN_FWD_WAVES_PER_SIMD
+#define HN_FWD_WAVES_PER_SIMD 3
+#endif
+// 3 waves per SIMD (<= 168 registers): the encode's gathers and the MFMA
+// chains of one ray overlap with two other rays' work
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
+void render_fwd_kernel(RenderK k) {
   __shared__ __attribute__((aligned(16))) float smem[kFwdWaves * kFLds + kGsLds];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
