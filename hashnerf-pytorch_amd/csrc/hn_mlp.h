@@ -295,5 +295,6 @@ HN_DEV float pack_value(const hn_mlp& w, int idx) {
 
 // Launch the packing kernel (hn_mlp.hip).
 int32_t mlp_pack_launch(const hn_mlp* w, float* packed, hipStream_t s);
+int32_t mlp_pack2_launch(const hn_mlp* w0, float* p0, const hn_mlp* w1, float* p1, hipStream_t s);
 
 }  // namespace hn

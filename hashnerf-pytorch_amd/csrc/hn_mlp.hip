@@ -115,6 +115,21 @@ static bool mlp_ok(const hn_mlp* w) {
 
 extern "C" size_t hn_mlp_workspace_bytes(void) { return (size_t)G_END * sizeof(float); }
 
+// Both networks of the renderer in one launch (blockIdx.y = network).
+__global__ __launch_bounds__(256) void mlp_pack2_kernel(hn_mlp w0, float* __restrict__ p0, hn_mlp w1,
+                                                        float* __restrict__ p1) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < G_END) {
+    if (blockIdx.y == 0) p0[idx] = pack_value(w0, idx);
+    else p1[idx] = pack_value(w1, idx);
+  }
+}
+
+int32_t hn::mlp_pack2_launch(const hn_mlp* w0, float* p0, const hn_mlp* w1, float* p1, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_pack2_kernel, dim3((G_END + 255) / 256, 2), dim3(256), 0, s, *w0, p0, *w1, p1);
+  return hip_status(hipGetLastError());
+}
+
 int32_t hn::mlp_pack_launch(const hn_mlp* w, float* packed, hipStream_t s) {
   hipLaunchKernelGGL(mlp_pack_kernel, dim3((G_END + 255) / 256), dim3(256), 0, s, *w, packed);
   return hip_status(hipGetLastError());

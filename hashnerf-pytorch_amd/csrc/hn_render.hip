@@ -999,8 +999,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   hipStream_t s = (hipStream_t)stream;
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
-  if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
-  if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
+  if ((st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   RenderK k;
   k.g = make_grid_args(cfg->grid);
   k.white = cfg->white_bkgd;
@@ -1037,10 +1036,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
   float* dfeat = slab + (size_t)kBwdBlocks * 2 * W_END;
-  if (!a->weights_packed) {
-    if ((st = mlp_pack_launch(&a->coarse, Pc, s))) return st;
-    if ((st = mlp_pack_launch(&a->fine, Pf, s))) return st;
-  }
+  if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   B1K k;
   k.B = a->n_rays;
   k.white = cfg->white_bkgd;

@@ -86,7 +86,23 @@ __global__ __launch_bounds__(kLossThreads) void loss_fwd_kernel(
     int n_tv, float world, float sparse_w, float tv_w, float* __restrict__ out) {
   __shared__ double red[4][kLossThreads / 64];
   double a[4] = {0.0, 0.0, 0.0, 0.0};   // sse, sse0, entropy, tv
-  for (int64_t j = threadIdx.x; j < 3 * n; j += kLossThreads) {
+  // float4 loads where the arrays are 16-B aligned (torch allocations are),
+  // every load of a thread in flight at once: one workgroup is launch-bound
+  const bool vec = ((reinterpret_cast<uintptr_t>(rgb) | reinterpret_cast<uintptr_t>(target) |
+                     reinterpret_cast<uintptr_t>(rgb0) | reinterpret_cast<uintptr_t>(sp) |
+                     reinterpret_cast<uintptr_t>(sp0)) & 15u) == 0;
+  const int64_t m3 = vec ? (3 * n) / 4 : 0, m1 = vec ? n / 4 : 0;
+  for (int64_t j = threadIdx.x; j < m3; j += kLossThreads) {
+    const float4 x = reinterpret_cast<const float4*>(rgb)[j], t = reinterpret_cast<const float4*>(target)[j];
+    const float e[4] = {x.x - t.x, x.y - t.y, x.z - t.z, x.w - t.w};
+    for (int q = 0; q < 4; ++q) a[0] += (double)(e[q] * e[q]);
+    if (rgb0) {
+      const float4 y = reinterpret_cast<const float4*>(rgb0)[j];
+      const float f[4] = {y.x - t.x, y.y - t.y, y.z - t.z, y.w - t.w};
+      for (int q = 0; q < 4; ++q) a[1] += (double)(f[q] * f[q]);
+    }
+  }
+  for (int64_t j = 4 * m3 + threadIdx.x; j < 3 * n; j += kLossThreads) {
     const float e = rgb[j] - target[j];
     a[0] += (double)(e * e);
     if (rgb0) {
@@ -94,7 +110,16 @@ __global__ __launch_bounds__(kLossThreads) void loss_fwd_kernel(
       a[1] += (double)(e0 * e0);
     }
   }
-  for (int64_t j = threadIdx.x; j < n; j += kLossThreads) a[2] += (double)sp[j] + (sp0 ? (double)sp0[j] : 0.0);
+  for (int64_t j = threadIdx.x; j < m1; j += kLossThreads) {
+    const float4 x = reinterpret_cast<const float4*>(sp)[j];
+    a[2] += ((double)x.x + (double)x.y) + ((double)x.z + (double)x.w);
+    if (sp0) {
+      const float4 y = reinterpret_cast<const float4*>(sp0)[j];
+      a[2] += ((double)y.x + (double)y.y) + ((double)y.z + (double)y.w);
+    }
+  }
+  for (int64_t j = 4 * m1 + threadIdx.x; j < n; j += kLossThreads)
+    a[2] += (double)sp[j] + (sp0 ? (double)sp0[j] : 0.0);
   if (tv)
     for (int j = threadIdx.x; j < n_tv; j += kLossThreads) a[3] += (double)tv[j];
 #pragma unroll
