@@ -13,7 +13,7 @@ import build
 defs = sys.argv[1].split()
 build.build_variant(defs, f"/tmp/hn_variant{sys.argv[2]}.so")
 PY
-  HN_LIB_PATH=/tmp/hn_variant$i.so timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline \
+  HN_LIB_PATH=/tmp/hn_variant$i.so timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS \
       > $OUT/variant$i.json 2> $OUT/variant$i.err || exit 1
   python -c "import json;d=json.load(open('$OUT/variant$i.json'));print('$V', d['value'], d['ms_per_step'], d['kernels'])"
 done
