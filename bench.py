@@ -41,7 +41,7 @@ UNIQUE_PTS = 192               # per ray (the 64 coarse points recur in the fine
 PATH_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2 + 36
 BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2        # bwd kernel: re-gather + scatter-add
 FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
-BWD_KERNELS = ("render_bwd_kernel", "slab_reduce_kernel")   # the hn_render_bwd launch
+BWD_KERNELS = ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel")   # hn_render_bwd
 
 
 def measured_traffic(cfg_id, n_rand_override):

@@ -61,6 +61,7 @@ struct B1K {
   const float* g_raw_f;
   float* slab;
   float* dfeat;         // [B][64][32] coarse-pass feature grads ([f][level] per point)
+  float* draw;          // [B][64 + 192][4] d raw of every sample (composite pre-pass)
   // fine kernel: trilinear backward + scatter into the table gradient
   GridArgs g;
   const uint8_t* fine_src;
@@ -293,17 +294,31 @@ void render_fwd_kernel(RenderK k) {
 // ds_read_b128 per operand.  ReLU masks are kept as bits.
 //
 // Work units: a coarse unit is one ray's 2 coarse tiles, a fine unit 2 of a
-// ray's 6 fine tiles (each fine unit redoes the ray's cheap composite
-// backward).  Wave 0 of every block runs coarse units, waves 1-3 fine units:
-// 1 : 3 matches the 2 : 6 tile ratio, so every wave gets the same tile count.
+// ray's 6 fine tiles.  Waves 0-2 run units (wave 0 first every coarse unit of
+// the block, then fine units with waves 1-2); wave 3 only scatters the fine
+// tiles' table gradients, handed over through an LDS ring.  The composite
+// backward (d raw per sample) comes from a full-occupancy pre-pass.
 // ---------------------------------------------------------------------------
 constexpr int kXS = 36;
 // image rows per wave: features | h0 | [sh16 | geo15] | c0 | c1 | rgb grads
 constexpr int kRF = 0, kRH0 = 32, kRC0in = 96, kRC0 = 128, kRC1 = 192, kRC2 = 256, kRRows = 260;
 constexpr int kB1Waves = 4;
-constexpr int kB1Lds = kB1Waves * kRRows * kXS;            // floats (149,760 B)
-static_assert(kB1Lds >= 2 * W_END, "final dW reduction reuses the images");
-static_assert(kRRows * kXS % 4 == 0 && kXS % 4 == 0, "b128 alignment");
+constexpr int kMW = kB1Waves - 1;                          // MLP waves; wave kMW scatters
+constexpr int kB1Img = kMW * kRRows * kXS;                 // floats (112,320 B)
+// Fine-tile hand-off ring (MLP waves -> scatter wave): per slot the tile's
+// feature grads [32 points][kXS] ([f][level], coarse twin added), the 32
+// sample depths and the ray origin / direction.
+#ifndef HN_SLOTS
+#define HN_SLOTS 8
+#endif
+constexpr int kSlots = HN_SLOTS;
+constexpr int kSlotZ = 32 * kXS, kSlotR = kSlotZ + 32, kSlotF = kSlotR + 8;
+constexpr int kVoxF = 16 * 16 * 8;                         // scatter wave's voxel buffer
+constexpr int kSyncInts = 4 + 2 * kSlots;
+constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + kGsLds + kSyncInts;
+static_assert(kB1LdsF * 4 <= 160 * 1024, "LDS budget");
+static_assert(kB1Img >= W_END, "final dW reduction reuses the images");
+static_assert(kRRows * kXS % 4 == 0 && kXS % 4 == 0 && kSlotF % 4 == 0, "b128 alignment");
 
 struct DW {
   f32x16 c2[2], c1[4], c0[2], s1[2], s0[2];
@@ -349,7 +364,11 @@ struct GemmSeg {
 constexpr GemmSeg kSegs[] = {{G_F0, 16, 0}, {G_F0, 16, 1}, {G_F1, 32, 0}, {G_F2G, 8, 0}, {G_F2G, 8, 1},
                              {G_F3, 32, 0}, {G_F3, 32, 1}, {G_B4, 4, 0},  {G_B4, 4, 1},  {G_B3, 32, 0},
                              {G_B3, 32, 1}, {G_B2G, 32, 0}, {G_B1, 8, 0}, {G_B1, 8, 1},  {G_B0, 32, 0}};
-constexpr int kTileGroups = 74, kRing = 4, kTilePeriod = 76;   // 2 pad groups
+#ifndef HN_WRING
+#define HN_WRING 4
+#endif
+constexpr int kTileGroups = 74, kRing = HN_WRING;
+constexpr int kTilePeriod = (kTileGroups + kRing - 1) / kRing * kRing;   // pad groups keep slots static
 constexpr int group_off(int idx) {
   idx %= kTilePeriod;
   if (idx >= kTileGroups) idx = 0;              // pad groups re-read group 0
@@ -507,8 +526,9 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   dw.s0[0] = wgrad(X, kRC0 + i, kRF + i, dw.s0[0], lane);
   dw.s0[1] = wgrad(X, kRC0 + 32 + i, kRF + i, dw.s0[1], lane);
   const f32x16 dfeat = gemm_w<32, 66>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
-  (void)wring_take<74>(wr, P, lane);            // pad groups: keep the ring aligned with the tile
-  (void)wring_take<75>(wr, P, lane);
+  static_for<kTileGroups, kTilePeriod - kTileGroups>([&](auto gc) {   // pad groups: keep the ring
+    (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
+  });
   lds_fence_wave();                             // image reads done before any later writes
   return dfeat;
 }
@@ -528,14 +548,15 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
 // the ray and sit along a 16-lane DPP row, so a run of samples inside one
 // voxel is summed by a segmented suffix sum of row shifts (no LDS round
 // trips, no branches) and only the run head issues atomics.
+// DPP row shifts; lanes whose source is outside the row read 0 (bound_ctrl),
+// which lets the compiler fold the shift into the consuming VALU op.
 template <int CTRL>
 HN_DEV uint32_t dpp_u(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
 }
 template <int CTRL>
 HN_DEV float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf,
-                                                    false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
 }
 constexpr int kRowShr1 = 0x111;              // lane i <- lane i-1 within its row
 template <int D> constexpr int kRowShl = 0x100 + D;   // lane i <- lane i+D within its row
@@ -556,18 +577,28 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
   }
 }
 
+// Atomic wave-instructions the scatter wave may have in flight before it
+// issues a level's 4 (-1: no cap).  Uncapped, its atomics crowd the CU's
+// vector-memory pipeline and the MLP waves' weight loads stall behind them
+// (backward 1.59 ms at config 2); capped too tightly, the scatter wave waits
+// on atomic latency.  Measured (scripts/variants.sh): 1: 1.59 ms, 2: 1.56,
+// 4: 1.496, 6: 1.508.
+#ifndef HN_SW_VMCNT
+#define HN_SW_VMCNT 4
+#endif
 // One level of the scatter for the 16 points of a pass; v = this lane's
-// point's voxel {cell x, y, z, w x, y, z} (from the compact pass via LDS).
+// point's voxel {cell x, cell y * PY, cell z * PZ, w x, y, z} from the compact
+// pass (the prime products are precomputed there: (c + 1) * P = c * P + P,
+// and c -> c * P is a bijection, so run heads compare the products).
 HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const f32x4 v0, const float2 v1,
                             uint32_t l, float gl, int lane) {
   const int pp = lane & 15, f = (lane >> 4) & 1, xi = lane >> 5;
-  const uint32_t cell[3] = {(uint32_t)__float_as_int(v0.x), (uint32_t)__float_as_int(v0.y),
-                            (uint32_t)__float_as_int(v0.z)};
+  const uint32_t cx = (uint32_t)__float_as_int(v0.x), y0 = (uint32_t)__float_as_int(v0.y),
+                 z0 = (uint32_t)__float_as_int(v0.z);
   const float w[3] = {v0.w, v1.x, v1.y};
   const uint32_t mask = (1u << g.log2T) - 1u;
-  const uint32_t hx = cell[0] + (uint32_t)xi;
-  const uint32_t y0 = cell[1] * kPrimeY, y1 = (cell[1] + 1u) * kPrimeY;
-  const uint32_t z0 = cell[2] * kPrimeZ, z1 = (cell[2] + 1u) * kPrimeZ;
+  const uint32_t hx = cx + (uint32_t)xi;
+  const uint32_t y1 = y0 + kPrimeY, z1 = z0 + kPrimeZ;
   // d feat / d e_c = ((g * fz) * fy) * fx  (trilerp_bwd order), c = 4*xi + jk
   const float fx = xi ? w[0] : 1.f - w[0];
   const float gz0 = gl * (1.f - w[2]), gz1 = gl * w[2];
@@ -576,12 +607,15 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
   cv[1] = (gz1 * (1.f - w[1])) * fx;   // j=0 k=1
   cv[2] = (gz0 * w[1]) * fx;           // j=1 k=0
   cv[3] = (gz1 * w[1]) * fx;           // j=1 k=1
-  const uint32_t q0 = dpp_u<kRowShr1>(cell[0]), q1 = dpp_u<kRowShr1>(cell[1]),
-                 q2 = dpp_u<kRowShr1>(cell[2]);
-  const bool head = pp == 0 || q0 != cell[0] || q1 != cell[1] || q2 != cell[2];
+  const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
+  const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
   const uint32_t pm = (uint32_t)__ballot(head) & 0xffffu;   // every row sees the same points
-  if (pm != 0xffffu) {                     // some run of >= 2 samples in one voxel
-    // lane p absorbs lane p+d iff no run starts in (p, p+d]
+  // Segmented suffix sum over runs of samples in one voxel: lane p absorbs
+  // lane p+d iff no run starts in (p, p+d].  Step d is only needed when some
+  // run is longer than d (k consecutive non-heads = a run of > k samples);
+  // the tests are on the wave-uniform head mask, so skipped steps cost nothing.
+  const uint32_t nz1 = ~pm & 0xfffeu;
+  if (nz1) {
     auto absorb = [&](auto dc, int d) {
       const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
 #pragma unroll
@@ -591,48 +625,15 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
       }
     };
     absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
-    absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
-    absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
-    absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
-  }
-  // Neighbour merge (same x row of corners): a run head shares the corners of
-  // the common face/edge with the adjacent run head when the cells differ by
-  // at most one in y and z.  Such a corner then costs one atomic, not two: the
-  // later point gives its contribution to the earlier one -- unless it also
-  // shares that corner with ITS successor (then it keeps it), which keeps the
-  // rule chain-free: every contribution is issued exactly once.  On recorded
-  // samples this removes ~11 % of the memory-side requests.
-  const bool prev_h = pp > 0 && ((pm >> (pp - 1)) & 1u);
-  const bool next_h = pp < 15 && ((pm >> (pp + 1)) & 1u);
-  const uint32_t n0 = dpp_u<kRowShl<1>>(cell[0]), n1 = dpp_u<kRowShl<1>>(cell[1]),
-                 n2 = dpp_u<kRowShl<1>>(cell[2]);
-  const int dny = (int)(n1 - cell[1]), dnz = (int)(n2 - cell[2]);
-  const int dpy = (int)(cell[1] - q1), dpz = (int)(cell[2] - q2);
-  const bool nok = head && next_h && n0 == cell[0], pok = head && prev_h && q0 == cell[0];
-  uint32_t rr = 0, pr = 0;   // corners (registers 2j+k) shared with the next / previous head
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = r >> 1, kk = r & 1;
-    if (nok && (unsigned)(j - dny) <= 1u && (unsigned)(kk - dnz) <= 1u) rr |= 1u << r;
-    if (pok && (unsigned)(j + dpy) <= 1u && (unsigned)(kk + dpz) <= 1u) pr |= 1u << r;
-  }
-// Measured (scripts/variants.sh): -9 % atomic requests but the extra VALU
-// makes the step 1.8 % slower at config 2 and equal at config 3 -> off.
-#ifndef HN_NEIGHBOUR_MERGE
-#define HN_NEIGHBOUR_MERGE 0
-#endif
-  const uint32_t give = HN_NEIGHBOUR_MERGE ? (pr & ~rr) : 0u;
-  if (!HN_NEIGHBOUR_MERGE) rr = 0u;
-  const uint32_t nrr = dpp_u<kRowShl<1>>(rr);   // the successor's "shares with its successor" mask
-  float ncv[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) ncv[c] = dpp_f<kRowShl<1>>(cv[c]);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rp = 2 * ((r >> 1) - dny) + ((r & 1) - dnz);   // successor's register of this corner
-    const bool take = ((rr >> r) & 1u) && !((nrr >> (rp & 3)) & 1u);
-    const float o = (rp & 2) ? ((rp & 1) ? ncv[3] : ncv[2]) : ((rp & 1) ? ncv[1] : ncv[0]);
-    cv[r] = take ? cv[r] + o : cv[r];
+    const uint32_t nz2 = nz1 & (nz1 >> 1);
+    if (nz2) {
+      absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
+      const uint32_t nz4 = nz2 & (nz2 >> 2);
+      if (nz4) {
+        absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
+        if (nz4 & (nz4 >> 4)) absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
+      }
+    }
   }
 #if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
   if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
@@ -641,92 +642,20 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     const uint32_t row0 = l << g.log2T;
     const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
                             (hx ^ y1 ^ z1) & mask};
+#if HN_SW_VMCNT >= 0
+    // cap the atomics in flight (they share the CU's vector-memory pipeline
+    // with the MLP waves' weight loads); waiting only here, after this
+    // level's VALU, overlaps the wait with it
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HN_SW_VMCNT) : "memory");
+#endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if ((give >> c) & 1u) continue;            // issued by the previous head
       float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
                                             (row0 + hh[c]) * 8u + 4u * f);
       atomic_add_f32(dst, cv[c]);
     }
   }
 #endif
-}
-
-HN_DEV void scatter_tile(const B1K& k, const float* gsl, float* X, const Ray& r, int64_t ray, int qbase,
-                         const f32x16& dfeat) {
-  const int lane = lane_id();
-  const int p = lane & 31, h = lane >> 5;
-  const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
-  // every global load of the phase is issued before its first atomic: a load
-  // behind outstanding atomics would wait for all of them (in-order vmcnt)
-  float zq[2], glc[2][16];
-  int srcq[2];
-#pragma unroll
-  for (int grp = 0; grp < 2; ++grp) {
-    const int q = qbase + 16 * grp + pp;
-    zq[grp] = k.z_fine[ray * kSf + q];
-    srcq[grp] = k.fine_src[ray * kSf + q];
-  }
-#pragma unroll
-  for (int grp = 0; grp < 2; ++grp) {
-    const bool twin = srcq[grp] < kSc;
-    const float4* dc = reinterpret_cast<const float4*>(
-        k.dfeat + ((size_t)ray * kSc + (twin ? srcq[grp] : 0)) * 32 + 16 * f);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float4 v = twin ? dc[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-      glc[grp][4 * c] = v.x; glc[grp][4 * c + 1] = v.y; glc[grp][4 * c + 2] = v.z; glc[grp][4 * c + 3] = v.w;
-    }
-  }
-  float* T = X + kRF * kXS;                     // [32 points][kXS]: [feature][level]
-  float* V = X + kRH0 * kXS;                    // [16 levels][16 points][8]: voxel of a pass
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int l = h ? tile_level(m, 1) : tile_level(m, 0);
-    T[p * kXS + l] = dfeat[2 * m];
-    T[p * kXS + 16 + l] = dfeat[2 * m + 1];
-  }
-#pragma unroll
-  for (int grp = 0; grp < 2; ++grp) {
-    float pt[3], xc[3];
-    ray_point(r, zq[grp], pt);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
-    // compact pass: lane (row lq, point pp) computes levels lq, lq+4, lq+8, lq+12
-    // once, instead of every (x offset, feature) row repeating the divisions
-    if (grp) lds_fence_wave();                  // previous pass's voxel reads done
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int l = 4 * b + lq;
-      int32_t cell[3];
-      float w[3];
-      voxel_cw(k.g, gsl, pt, xc, l, cell, w);
-      float* dst = V + (l * 16 + pp) * 8;
-      *reinterpret_cast<f32x4*>(dst) = f32x4{__int_as_float(cell[0]), __int_as_float(cell[1]),
-                                              __int_as_float(cell[2]), w[0]};
-      *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
-    }
-    lds_fence_wave();
-    float gl[16];
-    const f32x4* src4 = reinterpret_cast<const f32x4*>(T + (16 * grp + pp) * kXS + 16 * f);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const f32x4 v = src4[c];
-      // fine-pass grad + coarse twin's grad (zero when not a twin): the order
-      // of the former two-kernel scatter
-      gl[4 * c] = v.x + glc[grp][4 * c]; gl[4 * c + 1] = v.y + glc[grp][4 * c + 1];
-      gl[4 * c + 2] = v.z + glc[grp][4 * c + 2]; gl[4 * c + 3] = v.w + glc[grp][4 * c + 3];
-    }
-#pragma unroll
-    for (int l = 0; l < 16; ++l) {
-      const float* vs = V + (l * 16 + pp) * 8;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
-      const float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
-      scatter_level_x(k.g, k.d_table, v0, v1, l, gl[l], lane);
-      if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  lds_fence_wave();
 }
 
 // Diagnostic phase timers (HN_PROFILE builds only, scripts/b1_profile.sh):
@@ -751,9 +680,161 @@ struct PhaseClock {
 #if HN_PROFILE
 #define HN_LAP(pc, field) (pc).lap((pc).field)
 __device__ unsigned long long g_phase[2][8];
+// ring waits: [0] scatter wave total, [1] scatter wave waiting on ready,
+// [2] MLP waves waiting on a free slot, [3] MLP waves waiting on the coarse flag
+__device__ unsigned long long g_ring[4];
 #else
 #define HN_LAP(pc, field) ((void)0)
 #endif
+
+
+// ---- fine-tile hand-off ring ----------------------------------------------
+// The MLP waves never issue an atomic and the scatter wave never issues a
+// global load: a load behind outstanding atomics waits for all of them
+// (in-order vmcnt), so mixing the two in one wave exposes the atomic latency.
+// Protocol (LDS ints, single consumer): a producer takes ticket t, waits until
+// slot t % kSlots has been consumed t / kSlots times, fills it and publishes
+// ready[slot] = t + 1; the consumer takes tickets in order.  The producer
+// holding the oldest unconsumed ticket never waits, so the ring cannot
+// deadlock.  Flags are relaxed LDS atomics ordered by lgkmcnt(0) fences (an
+// acquire / release would also wait vmcnt(0), draining the atomics).
+struct Ring {
+  float* slots;
+  int* tick;    // next ticket
+  int* ready;   // [kSlots] ticket + 1 of the slot's contents
+  int* freed;   // [kSlots] times consumed
+};
+
+// Bounded spin on a workgroup-local flag (a protocol bug ends in wrong
+// results, never in a hung GPU).
+HN_DEV void spin_until(int* flag, int need, int prof_slot = -1) {
+#if HN_PROFILE
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  for (int it = 0; it < (1 << 22); ++it) {
+    const int v = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v >= need) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  asm volatile("" ::: "memory");
+#if HN_PROFILE
+  if (prof_slot >= 0 && lane_id() == 0)
+    atomicAdd(&g_ring[prof_slot], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+#endif
+}
+
+HN_DEV void ring_publish(int* flag, int v) {
+  lds_fence_wave();                               // the slot's LDS accesses are done
+  if (lane_id() == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Producer: one fine tile's feature grads (D layout), plus the coarse twin's
+// grads -- a fine sample that is one of the 64 coarse samples (fine_src < 64)
+// is the same point in both passes, so every unique point is scattered once.
+// z / src: this lane's point's sample depth and fine_src (prefetched per unit)
+HN_DEV void ring_put(const B1K& k, const Ring& q, const Ray& r, int64_t ray, float z, int src,
+                     const f32x16& dfeat) {
+  const int lane = lane_id();
+  const int p = lane & 31, h = lane >> 5;
+  const bool twin = src < kSc;
+  const f32x4* dc =
+      reinterpret_cast<const f32x4*>(k.dfeat + ((size_t)ray * kSc + (twin ? src : 0)) * 32 + 16 * h);
+  f32x4 tw[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) tw[c] = twin ? dc[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  int t = 0;
+  if (lane == 0) t = atomicAdd(q.tick, 1);
+  t = __builtin_amdgcn_readfirstlane(t);
+  const int s = t % kSlots;
+  spin_until(&q.freed[s], t / kSlots, 2);
+  float* S = q.slots + s * kSlotF;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int l = h ? tile_level(m, 1) : tile_level(m, 0);
+    S[p * kXS + l] = dfeat[2 * m];
+    S[p * kXS + 16 + l] = dfeat[2 * m + 1];
+  }
+  lds_fence_wave();
+  // lane (point p, feature h): fine grad + twin grad, the order of the former
+  // two-kernel scatter
+  f32x4* g4 = reinterpret_cast<f32x4*>(S + p * kXS + 16 * h);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) g4[c] = g4[c] + tw[c];
+  if (h == 0) S[kSlotZ + p] = z;
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      S[kSlotR + a] = r.o[a];
+      S[kSlotR + 3 + a] = r.d[a];
+    }
+  }
+  ring_publish(&q.ready[s], t + 1);
+}
+
+// Consumer: the table-gradient scatter of n_tiles fine tiles
+// (embedding_dense_backward of hash_encoding.py:106 + trilinear backward).
+HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, const float* gsl, int n_tiles) {
+  const int lane = lane_id();
+  const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
+  for (int t = 0; t < n_tiles; ++t) {
+    const int s = t % kSlots;
+    spin_until(&q.ready[s], t + 1, 1);
+    const float* S = q.slots + s * kSlotF;
+    Ray r;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      r.o[a] = S[kSlotR + a];
+      r.d[a] = S[kSlotR + 3 + a];
+    }
+#pragma unroll
+    for (int grp = 0; grp < 2; ++grp) {
+      float pt[3], xc[3];
+      ray_point(r, S[kSlotZ + 16 * grp + pp], pt);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
+      // compact pass: lane (row lq, point pp) computes levels lq, lq+4, lq+8,
+      // lq+12 once, instead of every (x offset, feature) row repeating the divisions
+      if (grp) lds_fence_wave();                // previous pass's voxel reads done
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int l = 4 * b + lq;
+        int32_t cell[3];
+        float w[3];
+        voxel_cw(k.g, gsl, pt, xc, l, cell, w);
+        float* dst = V + (l * 16 + pp) * 8;
+        *reinterpret_cast<f32x4*>(dst) = f32x4{__int_as_float(cell[0]), __uint_as_float((uint32_t)cell[1] * kPrimeY),
+                                                __uint_as_float((uint32_t)cell[2] * kPrimeZ), w[0]};
+        *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
+      }
+      lds_fence_wave();
+      float gl[16];
+      const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + 16 * f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f32x4 v = src4[c];
+        gl[4 * c] = v.x; gl[4 * c + 1] = v.y; gl[4 * c + 2] = v.z; gl[4 * c + 3] = v.w;
+      }
+      // voxel records are read one level ahead (one wave per SIMD: nothing
+      // else hides the LDS latency)
+      const float* vs = V + pp * 8;
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
+      float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
+#pragma unroll
+      for (int l = 0; l < 16; ++l) {
+        const f32x4 c0 = v0;
+        const float2 c1 = v1;
+        if (l < 15) {
+          v0 = *reinterpret_cast<const f32x4*>(vs + (l + 1) * 128);
+          v1 = *reinterpret_cast<const float2*>(vs + (l + 1) * 128 + 4);
+        }
+        scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane);
+        if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    ring_publish(&q.freed[s], t / kSlots + 1);   // also orders the voxel reads before the next writes
+  }
+}
 
 HN_DEV void wait_flag(int* flag, int need) {
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
@@ -761,20 +842,92 @@ HN_DEV void wait_flag(int* flag, int need) {
 }
 
 // One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
-// Fine units: before the first scatter, wait until the block's coarse wave has
-// published this ray's coarse feature grads (*done >= need)
+// Fine units hand each tile to the scatter wave; before the first hand-off
+// they wait until wave 0 has published this ray's coarse feature grads
+// (*done >= need)
 template <int S>
-HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const float* gsl,
+HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const Ring* ring,
                     PhaseClock& pc, int* done = nullptr, int need = 0) {
   pc.start();
   const int lane = lane_id();
-  constexpr int N = S / 64;
   constexpr bool fine = S == kSf;
   const int p = lane & 31, h = lane >> 5;
-  float* zb = X + kRC0 * kXS;                   // scratch over the c0 / c1 rows
-  float* rawb = zb + S;
   Ray r;
   load_ray(k.rays, ray, r);
+  const int tile0 = 2 * part;                   // tile within this pass
+  const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
+  float4 dr[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(drs + 128 * t);
+  float sh8[8], shx8[8];
+  ray_sh(r, h, sh8, shx8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) X[(kRC0in + 8 * h + j) * kXS + p] = shx8[j];
+  const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
+  // color_net.0 applied to the sh part: the same for every point of the ray
+  // (and bit-identical to starting each point's chain with it)
+  f32x16 c0sh[2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob)
+    c0sh[ob] = gemm<8>(P, G_F2S, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+  const int ctile = (fine ? kSc / 32 : 0) + tile0;
+  float zq[2] = {0.f, 0.f};
+  int srcq[2] = {0, 0};
+  if constexpr (fine) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      zq[t] = k.z_fine[ray * kSf + 32 * (tile0 + t) + p];
+      srcq[t] = k.fine_src[ray * kSf + 32 * (tile0 + t) + p];
+    }
+  }
+  f32x16 feat, featn;
+  load_feat(k.feat, ray, ctile, lane, feat);
+  load_feat(k.feat, ray, ctile + 1, lane, featn);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t == 0) HN_LAP(pc, unit);
+    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
+    HN_LAP(pc, mlp);
+    const int qbase = 32 * (tile0 + t);
+    if constexpr (fine) {
+#if HN_PROFILE
+      const uint64_t tw0 = __builtin_amdgcn_s_memtime();
+#endif
+      if (t == 0) wait_flag(done, need);       // the coarse twin grads are written
+#if HN_PROFILE
+      if (lane == 0) atomicAdd(&g_ring[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
+#endif
+      ring_put(k, *ring, r, ray, zq[t], srcq[t], dfeat);
+      HN_LAP(pc, scat);
+    } else {
+      // coarse: per-point feature grads [point][feature f][level] for the fine
+      // kernel's scatter (lane half h holds levels tile_level(m, h))
+      float* dst = k.dfeat + ((size_t)ray * kSc + qbase + p) * 32;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int l = h ? tile_level(m, 1) : tile_level(m, 0);
+        dst[l] = dfeat[2 * m];
+        dst[16 + l] = dfeat[2 * m + 1];
+      }
+    }
+  }
+}
+
+// Composite backward pre-pass (raw2outputs backward, run_nerf_helpers.py:577-628
+// via the :541 / :558 chain): one wave per (ray, pass) at full occupancy
+// writes d raw of every sample, so the MLP units only load one float4 per
+// point instead of each redoing the ray's scans.
+__global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
+  __shared__ float lds[kFwdWaves][kSf * 5];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
+  if (w >= 2 * k.B) return;
+  const int64_t ray = w >> 1;
+  const bool fine = (w & 1) != 0;
+  const int S = fine ? kSf : kSc;
+  float* zb = lds[wave];
+  float* rawb = zb + kSf;
   const float* zsrc = (fine ? k.z_fine : k.z_coarse) + ray * S;
   const float* rsrc = (fine ? k.raw_f : k.raw_c) + ray * S * 4;
   for (int j = lane; j < S; j += 64) {
@@ -782,6 +935,8 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
     *reinterpret_cast<float4*>(rawb + 4 * j) = *reinterpret_cast<const float4*>(rsrc + 4 * j);
   }
   lds_fence_wave();
+  Ray r;
+  load_ray(k.rays, ray, r);
   CompGrad g;
   const float* grgb = fine ? k.g_rgb : k.g_rgb0;
   const float* gacc = fine ? k.g_acc : k.g_acc0;
@@ -799,50 +954,14 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   const float* noise = fine ? (k.noise_f ? k.noise_f + ray * S : nullptr)
                             : (k.noise_c ? k.noise_c + ray * S : nullptr);
   const float* graw = (fine && k.g_raw_f) ? k.g_raw_f + ray * S * 4 : nullptr;
-  composite_bwd<N>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
+  float* dst = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0)) * 4;
+  if (fine)
+    composite_bwd<kSf / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
+  else
+    composite_bwd<kSc / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
   lds_fence_wave();
-  const int tile0 = 2 * part;                   // tile within this pass
-  float4 dr[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(rawb + 4 * (32 * (tile0 + t) + p));
-  float sh8[8], shx8[8];
-  ray_sh(r, h, sh8, shx8);
-  lds_fence_wave();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) X[(kRC0in + 8 * h + j) * kXS + p] = shx8[j];
-  const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
-  // color_net.0 applied to the sh part: the same for every point of the ray
-  // (and bit-identical to starting each point's chain with it)
-  f32x16 c0sh[2];
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob)
-    c0sh[ob] = gemm<8>(P, G_F2S, ob, zero16(), lane, [&](int s) { return sh8[s]; });
-  const int ctile = (fine ? kSc / 32 : 0) + tile0;
-  f32x16 feat, featn;
-  load_feat(k.feat, ray, ctile, lane, feat);
-  load_feat(k.feat, ray, ctile + 1, lane, featn);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if (t == 0) HN_LAP(pc, unit);
-    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
-    HN_LAP(pc, mlp);
-    const int qbase = 32 * (tile0 + t);
-    if constexpr (fine) {
-      if (t == 0) wait_flag(done, need);
-      scatter_tile(k, gsl, X, r, ray, qbase, dfeat);
-      HN_LAP(pc, scat);
-    } else {
-      // coarse: per-point feature grads [point][feature f][level] for the fine
-      // kernel's scatter (lane half h holds levels tile_level(m, h))
-      float* dst = k.dfeat + ((size_t)ray * kSc + qbase + p) * 32;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int l = h ? tile_level(m, 1) : tile_level(m, 0);
-        dst[l] = dfeat[2 * m];
-        dst[16 + l] = dfeat[2 * m + 1];
-      }
-    }
-  }
+  for (int j = lane; j < S; j += 64)
+    *reinterpret_cast<float4*>(dst + 4 * j) = *reinterpret_cast<const float4*>(rawb + 4 * j);
 }
 
 // acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS),
@@ -893,10 +1012,10 @@ HN_DEV void dw_zero(DW& dw) {
 // first runs the block's coarse units (MLP backward of network_fn only) and
 // publishes each ray's coarse feature grads through an LDS counter; then it
 // stores its coarse dW to the block's slab and joins the fine units.  Waves
-// 1-3 (and wave 0 once free) take fine units from an LDS work counter: MLP
-// backward of network_fine + the table-gradient scatter, waiting for the ray's
-// coarse grads (twin merge) before the first atomic.  The fine phase is bound
-// by the memory-side float-atomic rate, so the coarse MLP work runs under it.
+// 1-2 (and wave 0 once free) take fine units from an LDS work counter (MLP
+// backward of network_fine) and hand every fine tile's feature grads to
+// wave 3 through the LDS ring; wave 3 only scatters (the table gradient is
+// bound by the memory-side float-atomic rate, so the MLP work runs under it).
 // Every wave that waits, waits on a wave of its own workgroup: co-resident.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void render_bwd_kernel(B1K k) {
@@ -905,14 +1024,16 @@ void render_bwd_kernel(B1K k) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   float* X = smem + wave * kRRows * kXS;
-  float* gsl = smem + kB1Lds;
-  int* sync = reinterpret_cast<int*>(gsl + kGsLds);   // [0] coarse rays done, [1] fine units taken
+  float* slots = smem + kB1Img;
+  float* V = slots + kSlots * kSlotF;
+  float* gsl = V + kVoxF;
+  // [0] coarse rays done, [1] fine units taken, [2] ring tickets, [3] dW buffer zeroed,
+  // [4..) ready, freed
+  int* sync = reinterpret_cast<int*>(gsl + kGsLds);
   stage_grid_sizes(k.g, gsl);
-  if (threadIdx.x == 0) {
-    sync[0] = 0;
-    sync[1] = 0;
-  }
+  if (threadIdx.x < kSyncInts) sync[threadIdx.x] = 0;
   __syncthreads();
+  const Ring ring{slots, &sync[2], &sync[4], &sync[4 + kSlots]};
   const int64_t nb = gridDim.x;
   const int n_rays = k.B > (int64_t)blockIdx.x ? (int)((k.B - 1 - blockIdx.x) / nb + 1) : 0;
   DW dw;
@@ -922,26 +1043,42 @@ void render_bwd_kernel(B1K k) {
 #if HN_PROFILE
   const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #endif
-  if (wave == 0) {
-    wring_prime(wr, k.Pc, lane);
-    for (int i = 0; i < n_rays; ++i) {
-      b1_unit<kSc>(k, blockIdx.x + i * nb, 0, X, dw, wr, gsl, pc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this ray's feature grads are in L2
-      if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (wave == kMW) {
+    ring_drain(k, ring, V, gsl, 2 * kSf / 64 * n_rays);
+#if HN_PROFILE
+    if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
+#endif
+  } else {
+    if (wave == 0) {
+      wring_prime(wr, k.Pc, lane);
+      for (int i = 0; i < n_rays; ++i) {
+        b1_unit<kSc>(k, blockIdx.x + i * nb, 0, X, dw, wr, nullptr, pc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this ray's feature grads are in L2
+        if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      dw_flush<true>(dw, k.slab + (size_t)blockIdx.x * 2 * W_END, lane);
+      dw_zero(dw);
     }
-    dw_flush<true>(dw, k.slab + (size_t)blockIdx.x * 2 * W_END, lane);
-    dw_zero(dw);
-  }
-  wring_prime(wr, k.Pf, lane);
-  for (;;) {
-    int u = 0;
-    if (lane == 0) u = atomicAdd(&sync[1], 1);
-    u = __builtin_amdgcn_readfirstlane(u);
-    if (u >= 3 * n_rays) break;
-    b1_unit<kSf>(k, blockIdx.x + (int64_t)(u / 3) * nb, u % 3, X, dw, wr, gsl, pc, &sync[0], u / 3 + 1);
+    wring_prime(wr, k.Pf, lane);
+    for (;;) {
+      int u = 0;
+      if (lane == 0) u = atomicAdd(&sync[1], 1);
+      u = __builtin_amdgcn_readfirstlane(u);
+      if (u >= 3 * n_rays) break;
+      b1_unit<kSf>(k, blockIdx.x + (int64_t)(u / 3) * nb, u % 3, X, dw, wr, &ring, pc, &sync[0], u / 3 + 1);
+    }
+    // block reduction of the MLP waves' fine dW into wave 0's image, inside
+    // this branch: the accumulators must not be live in the scatter wave's
+    // code (a spill there would wait vmcnt(0), i.e. drain its atomics)
+    if (wave == 0) {
+      for (int j = lane; j < W_END; j += 64) smem[j] = 0.f;
+      ring_publish(&sync[3], 1);
+    }
+    spin_until(&sync[3], 1);
+    dw_flush<false>(dw, smem, lane);
   }
 #if HN_PROFILE
-  if (lane == 0) {
+  if (lane == 0 && wave < kMW) {
     const int role = wave == 0 ? 0 : 1;
     atomicAdd(&g_phase[role][0], (unsigned long long)pc.unit);
     atomicAdd(&g_phase[role][1], (unsigned long long)pc.mlp);
@@ -950,11 +1087,6 @@ void render_bwd_kernel(B1K k) {
     atomicAdd(&g_phase[role][4], 1ull);
   }
 #endif
-  // block reduction of the waves' fine dW into LDS, then the block's fine slab
-  __syncthreads();
-  for (int j = threadIdx.x; j < W_END; j += blockDim.x) smem[j] = 0.f;
-  __syncthreads();
-  dw_flush<false>(dw, smem, lane);
   __syncthreads();
   float* slab = k.slab + ((size_t)blockIdx.x * 2 + 1) * W_END;
   for (int j = threadIdx.x; j < W_END; j += blockDim.x) slab[j] = smem[j];
@@ -1013,11 +1145,12 @@ static bool grad_ok(const hn_mlp_grad& w) {
 using namespace hn;
 
 // Workspace: packed coarse + fine weights | dW slabs [256][2][9344] |
-// coarse-pass feature grads [n_rays][64][32].
+// coarse-pass feature grads [n_rays][64][32] | d raw [n_rays][256][4].
 extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays) {
   (void)cfg;
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
-  return ((size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32) * sizeof(float);
+  return ((size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32 + n * (kSc + kSf) * 4) *
+         sizeof(float);
 }
 
 extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
@@ -1076,6 +1209,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
   float* dfeat = slab + (size_t)kBwdBlocks * 2 * W_END;
+  float* draw = dfeat + (size_t)a->n_rays * kSc * 32;
   if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   B1K k;
   k.B = a->n_rays;
@@ -1089,23 +1223,33 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.g_sparsity0 = a->g_sparsity0; k.g_raw_f = a->g_raw_f;
   k.slab = slab;
   k.dfeat = dfeat;
+  k.draw = draw;
   k.g = make_grid_args(cfg->grid);
   k.fine_src = a->fine_src;
   k.d_table = a->d_table;
-  const size_t lds = (size_t)(kB1Lds + kGsLds + 4) * sizeof(float);
+  hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
+                     dim3(64 * kFwdWaves), 0, s, k);
+  const size_t lds = (size_t)kB1LdsF * sizeof(float);
   hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
 #if HN_PROFILE
   {
     unsigned long long ph[2][8];
-    hipStreamSynchronize(s);
-    hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
     for (int f = 0; f < 2; ++f)
       fprintf(stderr, "hn_b1_profile %s waves=%llu cycles/wave: unit %.0f mlp %.0f scatter %.0f total %.0f\n",
-              f ? "waves1-3" : "wave0", ph[f][4], (double)ph[f][0] / ph[f][4], (double)ph[f][1] / ph[f][4],
+              f ? "waves1-2" : "wave0", ph[f][4], (double)ph[f][0] / ph[f][4], (double)ph[f][1] / ph[f][4],
               (double)ph[f][2] / ph[f][4], (double)ph[f][3] / ph[f][4]);
     memset(ph, 0, sizeof(ph));
-    hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph));
+    unsigned long long rg[4];
+    (void)hipMemcpyFromSymbol(rg, HIP_SYMBOL(g_ring), sizeof(rg));
+    fprintf(stderr, "hn_b1_ring per block: scatter wave total %.0f waiting %.0f | MLP waves slot-wait %.0f "
+            "coarse-wait %.0f (per wave)\n", rg[0] / 256., rg[1] / 256., rg[2] / (256. * kMW),
+            rg[3] / (256. * kMW));
+    memset(rg, 0, sizeof(rg));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ring), rg, sizeof(rg));
   }
 #endif
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(256), 0, s, slab, kBwdBlocks,
