@@ -159,10 +159,21 @@ constexpr int kFZc = 0, kFZsrc = 64, kFZs = 256, kFRaw = 448, kFW = 1216, kFBins
               kFCdf = 1344, kFLds = 1408;
 
 #ifndef HN_FWD_WAVES_PER_SIMD
-#define HN_FWD_WAVES_PER_SIMD 3
+#define HN_FWD_WAVES_PER_SIMD 4
 #endif
-// 3 waves per SIMD (<= 168 registers): the encode's gathers and the MFMA
-// chains of one ray overlap with two other rays' work
+// 4 waves per SIMD (<= 128 registers; the few spills sit outside the tile
+// loops): one ray per wave, so a 4096-ray batch is exactly one round on 256
+// CUs (3 waves: 0.427 ms, a 1/3-occupied second round; 4: 0.418 ms)
+
+// Diagnostic phase timers of the forward (HN_PROFILE builds): cycles per wave
+// in [0] coarse encode, [1] coarse MLP, [2] composite + sampling + sort,
+// [3] fine encode, [4] fine MLP, [5] final composite, [6] total, [7] waves
+#if HN_PROFILE
+__device__ unsigned long long g_fwd[8];
+#define HN_FT(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); ft[i] += n_ - t_; t_ = n_; } while (0)
+#else
+#define HN_FT(i) ((void)0)
+#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
 void render_fwd_kernel(RenderK k) {
   __shared__ __attribute__((aligned(16))) float smem[kFwdWaves * kFLds + kGsLds];
@@ -184,6 +195,11 @@ void render_fwd_kernel(RenderK k) {
   float* cdf = L + kFCdf;
   Ray r;
   load_ray(k.rays, ray, r);
+#if HN_PROFILE
+  uint64_t ft[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+  uint64_t t_ = t0_;
+#endif
 
   // ---- coarse z_vals (:514-536) ----
   auto zlin = [&](int i) {
@@ -215,6 +231,7 @@ void render_fwd_kernel(RenderK k) {
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
     if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
+    HN_FT(0);
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
@@ -223,6 +240,7 @@ void render_fwd_kernel(RenderK k) {
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
       *reinterpret_cast<float4*>(k.raw_c + (ray * kSc + q) * 4) = o4;
     }
+    HN_FT(1);
   }
   lds_fence_wave();
   CompOut co;
@@ -250,6 +268,7 @@ void render_fwd_kernel(RenderK k) {
   }
   rank_sort_wave(zsrc, zs, kSf, lane, k.fine_src + ray * kSf, kSc);
   for (int i = lane; i < kSf; i += 64) k.z_fine[ray * kSf + i] = zs[i];
+  HN_FT(2);
 
   // ---- fine network (:556) ----
   for (int tau = 0; tau < kSf / 32; ++tau) {
@@ -260,6 +279,7 @@ void render_fwd_kernel(RenderK k) {
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
     if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
+    HN_FT(3);
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
@@ -268,6 +288,7 @@ void render_fwd_kernel(RenderK k) {
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
       *reinterpret_cast<float4*>(k.raw_f + (ray * kSf + q) * 4) = o4;
     }
+    HN_FT(4);
   }
   lds_fence_wave();
   CompOut fo;
@@ -280,6 +301,13 @@ void render_fwd_kernel(RenderK k) {
     k.acc[ray] = fo.acc;
     k.sparsity[ray] = fo.entropy;
   }
+#if HN_PROFILE
+  HN_FT(5);
+  ft[6] = __builtin_amdgcn_s_memtime() - t0_;
+  ft[7] = 1;
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_fwd[i], (unsigned long long)ft[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1188,6 +1216,19 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdWaves - 1) / kFwdWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdWaves), 0, s, k);
+#if HN_PROFILE
+  {
+    unsigned long long f[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_fwd), sizeof(f));
+    const double w = f[7] ? (double)f[7] : 1.;
+    fprintf(stderr, "hn_fwd_profile cycles/wave: coarse encode %.0f mlp %.0f | sample %.0f | fine encode %.0f "
+            "mlp %.0f | composite %.0f | total %.0f\n", f[0] / w, f[1] / w, f[2] / w, f[3] / w, f[4] / w,
+            f[5] / w, f[6] / w);
+    memset(f, 0, sizeof(f));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd), f, sizeof(f));
+  }
+#endif
   return hip_status(hipGetLastError());
 }
 
