@@ -342,7 +342,7 @@ constexpr int kB1Img = kMW * kRRows * kXS;                 // floats (112,320 B)
 constexpr int kSlots = HN_SLOTS;
 constexpr int kSlotZ = 32 * kXS, kSlotR = kSlotZ + 32, kSlotF = kSlotR + 8;
 constexpr int kVoxF = 16 * 16 * 8;                         // scatter wave's voxel buffer
-constexpr int kSyncInts = 4 + 2 * kSlots;
+constexpr int kSyncInts = 5 + 2 * kSlots;
 constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + kGsLds + kSyncInts;
 static_assert(kB1LdsF * 4 <= 160 * 1024, "LDS budget");
 static_assert(kB1Img >= W_END, "final dW reduction reuses the images");
@@ -611,6 +611,12 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 // (backward 1.59 ms at config 2); capped too tightly, the scatter wave waits
 // on atomic latency.  Measured (scripts/variants.sh): 1: 1.59 ms, 2: 1.56,
 // 4: 1.496, 6: 1.508.
+#ifndef HN_NMERGE
+#define HN_NMERGE 0
+#endif
+#ifndef HN_SPLIT_INSTR
+#define HN_SPLIT_INSTR 0
+#endif
 #ifndef HN_SW_VMCNT
 #define HN_SW_VMCNT 4
 #endif
@@ -642,27 +648,67 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
   // lane p+d iff no run starts in (p, p+d].  Step d is only needed when some
   // run is longer than d (k consecutive non-heads = a run of > k samples);
   // the tests are on the wave-uniform head mask, so skipped steps cost nothing.
-  const uint32_t nz1 = ~pm & 0xfffeu;
-  if (nz1) {
+  const uint32_t nz1 = ~pm & 0xfffeu, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
+  auto seg_sum = [&](float (&v)[4]) {
+    if (!nz1) return;
     auto absorb = [&](auto dc, int d) {
       const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float o = dpp_f<decltype(dc)::value>(cv[c]);
-        cv[c] = same ? cv[c] + o : cv[c];
+        const float o = dpp_f<decltype(dc)::value>(v[c]);
+        v[c] = same ? v[c] + o : v[c];
       }
     };
     absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
-    const uint32_t nz2 = nz1 & (nz1 >> 1);
     if (nz2) {
       absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
-      const uint32_t nz4 = nz2 & (nz2 >> 2);
       if (nz4) {
         absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
         if (nz4 & (nz4 >> 4)) absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
       }
     }
+  };
+  seg_sum(cv);
+  // Neighbour merge: consecutive run heads along the ray are usually
+  // adjacent voxels.  After a y/z step a head shares the corner rows (register
+  // c = 2j+k, both x lanes) of the common face with the previous head.  Heads
+  // with an odd index give those rows to the previous head, which has an even
+  // index and never gives, so no contribution is ever passed on twice.  The
+  // previous run's cell is the previous lane's (q0..q2); the given values move
+  // one lane down (into the receiver's run) and a second segmented sum brings
+  // them to the receiving head: DPP only, no LDS round trips.  -15 % memory-
+  // side requests on recorded samples (scripts/request_model.py).
+  uint32_t gfin = 0u;   // rows this lane gives away
+#if HN_NMERGE
+  {
+    const uint32_t hidx = (uint32_t)__builtin_popcount(pm & ((1u << pp) - 1u));
+    const uint32_t yp = y0 - q1 == kPrimeY, ym = q1 - y0 == kPrimeY;
+    const uint32_t zp = z0 - q2 == kPrimeZ, zm = q2 - z0 == kPrimeZ;
+    const bool ystill = y0 == q1, zstill = z0 == q2;
+    const bool yz = head && (hidx & 1u) && cx == q0 && (ystill || yp || ym) && (zstill || zp || zm) &&
+                    !(ystill && zstill);
+    // rows given: j = 0 after +y (my j=0 face is its j=1 face), j = 1 after -y
+    const uint32_t jm = 3u - 2u * yp - ym, km = 3u - 2u * zp - zm;
+    gfin = yz ? (km * (jm & 1u) | (km << 2) * (jm >> 1)) : 0u;
+    // the receiver's row c = (j, k) takes my row (j - dy, k - dz), i.e. row
+    // c ^ (2 [dy != 0] + [dz != 0]) when that is a given row: two selects, no
+    // index arithmetic (a select chain on an index becomes branches)
+    float s1[4], t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s1[c] = (zp | zm) ? cv[c ^ 1] : cv[c];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float v = (yp | ym) ? s1[c ^ 2] : s1[c];
+      const uint32_t j = (uint32_t)c >> 1, kk = (uint32_t)c & 1u;
+      // receiver row valid: after +y only its j=1 row, after -y only j=0
+      const bool ok = yz && (yp ? j == 1u : (ym ? j == 0u : true)) && (zp ? kk == 1u : (zm ? kk == 0u : true));
+      t[c] = dpp_f<kRowShl<1>>(ok ? v : 0.f);  // into the last lane of the receiver's run
+    }
+    seg_sum(t);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) cv[c] = cv[c] + t[c];
   }
+#endif
 #if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
   if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
 #else
@@ -676,12 +722,28 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     // level's VALU, overlaps the wait with it
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HN_SW_VMCNT) : "memory");
 #endif
+#if HN_SPLIT_INSTR   // diagnostic: the same requests in twice the wave-instructions
+    for (int half = 0; half < 2; ++half) {
+      if ((pp >> 3) == half) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if ((gfin >> c) & 1u) continue;
+          float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
+                                                (row0 + hh[c]) * 8u + 4u * f);
+          atomic_add_f32(dst, cv[c]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+      if ((gfin >> c) & 1u) continue;           // given to the previous head
       float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
                                             (row0 + hh[c]) * 8u + 4u * f);
       atomic_add_f32(dst, cv[c]);
     }
+#endif
   }
 #endif
 }
@@ -729,8 +791,10 @@ __device__ unsigned long long g_ring[4];
 struct Ring {
   float* slots;
   int* tick;    // next ticket
+  int* selfc;   // tiles an MLP wave scattered itself (ring full)
   int* ready;   // [kSlots] ticket + 1 of the slot's contents
   int* freed;   // [kSlots] times consumed
+  const float* gsl;
 };
 
 // Bounded spin on a workgroup-local flag (a protocol bug ends in wrong
@@ -752,31 +816,20 @@ HN_DEV void spin_until(int* flag, int need, int prof_slot = -1) {
 #endif
 }
 
+HN_DEV int lds_load(int* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
 HN_DEV void ring_publish(int* flag, int v) {
   lds_fence_wave();                               // the slot's LDS accesses are done
   if (lane_id() == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Producer: one fine tile's feature grads (D layout), plus the coarse twin's
-// grads -- a fine sample that is one of the 64 coarse samples (fine_src < 64)
-// is the same point in both passes, so every unique point is scattered once.
-// z / src: this lane's point's sample depth and fine_src (prefetched per unit)
-HN_DEV void ring_put(const B1K& k, const Ring& q, const Ray& r, int64_t ray, float z, int src,
-                     const f32x16& dfeat) {
+// A slot: the tile's feature grads [32 points][kXS] ([f][level]), the coarse
+// twin's grads added (tw, lane (point, feature h)), depths and the ray.
+HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, const f32x4 tw[4]) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
-  const bool twin = src < kSc;
-  const f32x4* dc =
-      reinterpret_cast<const f32x4*>(k.dfeat + ((size_t)ray * kSc + (twin ? src : 0)) * 32 + 16 * h);
-  f32x4 tw[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) tw[c] = twin ? dc[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-  int t = 0;
-  if (lane == 0) t = atomicAdd(q.tick, 1);
-  t = __builtin_amdgcn_readfirstlane(t);
-  const int s = t % kSlots;
-  spin_until(&q.freed[s], t / kSlots, 2);
-  float* S = q.slots + s * kSlotF;
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     const int l = h ? tile_level(m, 1) : tile_level(m, 0);
@@ -784,8 +837,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, const Ray& r, int64_t ray, flo
     S[p * kXS + 16 + l] = dfeat[2 * m + 1];
   }
   lds_fence_wave();
-  // lane (point p, feature h): fine grad + twin grad, the order of the former
-  // two-kernel scatter
+  // fine grad + twin grad: the order of the former two-kernel scatter
   f32x4* g4 = reinterpret_cast<f32x4*>(S + p * kXS + 16 * h);
 #pragma unroll
   for (int c = 0; c < 4; ++c) g4[c] = g4[c] + tw[c];
@@ -797,70 +849,135 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, const Ray& r, int64_t ray, flo
       S[kSlotR + 3 + a] = r.d[a];
     }
   }
+  lds_fence_wave();
+}
+
+// The table-gradient scatter of one slot (embedding_dense_backward of
+// hash_encoding.py:106 + trilinear backward); V = 2048-float voxel buffer.
+HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl) {
+  const int lane = lane_id();
+  const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
+  Ray r;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    r.o[a] = S[kSlotR + a];
+    r.d[a] = S[kSlotR + 3 + a];
+  }
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    float pt[3], xc[3];
+    ray_point(r, S[kSlotZ + 16 * grp + pp], pt);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
+    // compact pass: lane (row lq, point pp) computes levels lq, lq+4, lq+8,
+    // lq+12 once, instead of every (x offset, feature) row repeating the divisions
+    if (grp) lds_fence_wave();                  // previous pass's voxel reads done
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int l = 4 * b + lq;
+      int32_t cell[3];
+      float w[3];
+      voxel_cw(k.g, gsl, pt, xc, l, cell, w);
+      float* dst = V + (l * 16 + pp) * 8;
+      *reinterpret_cast<f32x4*>(dst) = f32x4{__int_as_float(cell[0]), __uint_as_float((uint32_t)cell[1] * kPrimeY),
+                                              __uint_as_float((uint32_t)cell[2] * kPrimeZ), w[0]};
+      *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
+    }
+    lds_fence_wave();
+    float gl[16];
+    const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + 16 * f);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 v = src4[c];
+      gl[4 * c] = v.x; gl[4 * c + 1] = v.y; gl[4 * c + 2] = v.z; gl[4 * c + 3] = v.w;
+    }
+    // voxel records are read one level ahead (one wave per SIMD: nothing
+    // else hides the LDS latency)
+    const float* vs = V + pp * 8;
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
+    float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+      const f32x4 c0 = v0;
+      const float2 c1 = v1;
+      if (l < 15) {
+        v0 = *reinterpret_cast<const f32x4*>(vs + (l + 1) * 128);
+        v1 = *reinterpret_cast<const float2*>(vs + (l + 1) * 128 + 4);
+      }
+      scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane);
+      if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  lds_fence_wave();                             // slot and voxel reads done
+}
+
+// Producer: one fine tile.  A fine sample that is one of the 64 coarse
+// samples (fine_src < 64) is the same point in both passes: its coarse-pass
+// grads are added, so every unique point is scattered once.  z / src: this
+// lane's point's depth and fine_src (prefetched per unit).  When the ring is
+// full (the scatter wave is behind), the MLP wave scatters the tile itself in
+// its own image region X (free between tiles) instead of waiting; its next
+// global load then waits for those atomics once.
+#ifndef HN_MW_SELF
+#define HN_MW_SELF 0
+#endif
+HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_t ray, float z, int src,
+                     const f32x16& dfeat) {
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const bool twin = src < kSc;
+  const f32x4* dc =
+      reinterpret_cast<const f32x4*>(k.dfeat + ((size_t)ray * kSc + (twin ? src : 0)) * 32 + 16 * h);
+  f32x4 tw[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) tw[c] = twin ? dc[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (HN_MW_SELF) {
+    const int tn = lds_load(q.tick);
+    if (lds_load(&q.freed[tn % kSlots]) < tn / kSlots) {   // next slot still occupied
+      if (lane == 0) atomicAdd(q.selfc, 1);
+      fill_slot(X, r, z, dfeat, tw);
+      scatter_slot(k, X, X + kSlotF, q.gsl);
+      return;
+    }
+  }
+  int t = 0;
+  if (lane == 0) t = atomicAdd(q.tick, 1);
+  t = __builtin_amdgcn_readfirstlane(t);
+  const int s = t % kSlots;
+  spin_until(&q.freed[s], t / kSlots, 2);
+  float* S = q.slots + s * kSlotF;
+  fill_slot(S, r, z, dfeat, tw);
   ring_publish(&q.ready[s], t + 1);
 }
 
-// Consumer: the table-gradient scatter of n_tiles fine tiles
-// (embedding_dense_backward of hash_encoding.py:106 + trilinear backward).
-HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, const float* gsl, int n_tiles) {
-  const int lane = lane_id();
-  const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
-  for (int t = 0; t < n_tiles; ++t) {
+// Consumer: takes tickets in order until every one of the n_tiles fine tiles
+// is accounted for (a ticket, or scattered by its MLP wave).  tick and selfc
+// only grow and a tile is counted before it is handled, so tick + selfc ==
+// n_tiles with t >= tick means no ticket t will ever come.
+HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
+  for (int t = 0;; ++t) {
     const int s = t % kSlots;
-    spin_until(&q.ready[s], t + 1, 1);
+#if HN_PROFILE
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+    bool have = false;
+    for (int it = 0; it < (1 << 22); ++it) {
+      if (lds_load(&q.ready[s]) >= t + 1) {
+        have = true;
+        break;
+      }
+      const int tk = lds_load(q.tick);
+      if (tk + lds_load(q.selfc) >= n_tiles && t >= tk) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    asm volatile("" ::: "memory");
+#if HN_PROFILE
+    if (lane_id() == 0) atomicAdd(&g_ring[1], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+#endif
+    if (!have) break;
     const float* S = q.slots + s * kSlotF;
-    Ray r;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      r.o[a] = S[kSlotR + a];
-      r.d[a] = S[kSlotR + 3 + a];
-    }
-#pragma unroll
-    for (int grp = 0; grp < 2; ++grp) {
-      float pt[3], xc[3];
-      ray_point(r, S[kSlotZ + 16 * grp + pp], pt);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
-      // compact pass: lane (row lq, point pp) computes levels lq, lq+4, lq+8,
-      // lq+12 once, instead of every (x offset, feature) row repeating the divisions
-      if (grp) lds_fence_wave();                // previous pass's voxel reads done
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int l = 4 * b + lq;
-        int32_t cell[3];
-        float w[3];
-        voxel_cw(k.g, gsl, pt, xc, l, cell, w);
-        float* dst = V + (l * 16 + pp) * 8;
-        *reinterpret_cast<f32x4*>(dst) = f32x4{__int_as_float(cell[0]), __uint_as_float((uint32_t)cell[1] * kPrimeY),
-                                                __uint_as_float((uint32_t)cell[2] * kPrimeZ), w[0]};
-        *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
-      }
-      lds_fence_wave();
-      float gl[16];
-      const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + 16 * f);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const f32x4 v = src4[c];
-        gl[4 * c] = v.x; gl[4 * c + 1] = v.y; gl[4 * c + 2] = v.z; gl[4 * c + 3] = v.w;
-      }
-      // voxel records are read one level ahead (one wave per SIMD: nothing
-      // else hides the LDS latency)
-      const float* vs = V + pp * 8;
-      f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
-      float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
-#pragma unroll
-      for (int l = 0; l < 16; ++l) {
-        const f32x4 c0 = v0;
-        const float2 c1 = v1;
-        if (l < 15) {
-          v0 = *reinterpret_cast<const f32x4*>(vs + (l + 1) * 128);
-          v1 = *reinterpret_cast<const float2*>(vs + (l + 1) * 128 + 4);
-        }
-        scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane);
-        if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    ring_publish(&q.freed[s], t / kSlots + 1);   // also orders the voxel reads before the next writes
+    scatter_slot(k, S, V, q.gsl);
+    ring_publish(&q.freed[s], t / kSlots + 1);
   }
 }
 
@@ -925,7 +1042,7 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 #if HN_PROFILE
       if (lane == 0) atomicAdd(&g_ring[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
 #endif
-      ring_put(k, *ring, r, ray, zq[t], srcq[t], dfeat);
+      ring_put(k, *ring, X, r, ray, zq[t], srcq[t], dfeat);
       HN_LAP(pc, scat);
     } else {
       // coarse: per-point feature grads [point][feature f][level] for the fine
@@ -1056,12 +1173,12 @@ void render_bwd_kernel(B1K k) {
   float* V = slots + kSlots * kSlotF;
   float* gsl = V + kVoxF;
   // [0] coarse rays done, [1] fine units taken, [2] ring tickets, [3] dW buffer zeroed,
-  // [4..) ready, freed
+  // [4] self-scattered tiles, [5..) ready, freed
   int* sync = reinterpret_cast<int*>(gsl + kGsLds);
   stage_grid_sizes(k.g, gsl);
   if (threadIdx.x < kSyncInts) sync[threadIdx.x] = 0;
   __syncthreads();
-  const Ring ring{slots, &sync[2], &sync[4], &sync[4 + kSlots]};
+  const Ring ring{slots, &sync[2], &sync[4], &sync[5], &sync[5 + kSlots], gsl};
   const int64_t nb = gridDim.x;
   const int n_rays = k.B > (int64_t)blockIdx.x ? (int)((k.B - 1 - blockIdx.x) / nb + 1) : 0;
   DW dw;
@@ -1072,7 +1189,7 @@ void render_bwd_kernel(B1K k) {
   const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #endif
   if (wave == kMW) {
-    ring_drain(k, ring, V, gsl, 2 * kSf / 64 * n_rays);
+    ring_drain(k, ring, V, 2 * kSf / 64 * n_rays);
 #if HN_PROFILE
     if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
 #endif

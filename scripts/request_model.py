@@ -86,6 +86,55 @@ def model(rays, z, bmin, bmax, log2T=19):
                                     cur.append(adr)
                                     if not (xi == 0 and p in xadj):
                                         xm.append(adr)
+                        # general neighbour give (prev head, any distance), y/z rows,
+                        # chain-free + x-step duplicate merge
+                        gm = []
+                        for idx, p in enumerate(heads):
+                            x, y, zz = (int(v) for v in cg[p])
+                            give_row = False
+                            xdup = False
+                            if idx > 0:
+                                q = heads[idx - 1]
+                                dx, dy, dz = (int(cg[p][a]) - int(cg[q][a]) for a in range(3))
+                                if dx == 0 and 0 <= j + dy <= 1 and 0 <= k + dz <= 1 and (dy or dz):
+                                    give_row = True
+                                if dx == 1 and dy == 0 and dz == 0:
+                                    xdup = True
+                            if give_row and idx + 1 < len(heads):
+                                r2 = heads[idx + 1]
+                                ex, ey, ez = (int(cg[r2][a]) - int(cg[p][a]) for a in range(3))
+                                # p receives into row (j,k) from r2 when r2's row (j-ey, k-ez) maps here
+                                if ex == 0 and (ey or ez) and 0 <= j - ey <= 1 and 0 <= k - ez <= 1:
+                                    give_row = False
+                            if give_row:
+                                continue
+                            hy = np.uint32((y + j) * int(PY) & 0xffffffff)
+                            hz = np.uint32((zz + k) * int(PZ) & 0xffffffff)
+                            for xi in (0, 1):
+                                if xi == 0 and xdup:
+                                    continue
+                                e = int((np.uint32(x + xi) ^ hy ^ hz) & mask)
+                                for f in (0, 1):
+                                    gm.append((row0 + e) * 2 + f)
+                        tot["general_give_merge"] += instr_cost(gm)[0] if gm else 0
+                        # parity rule: heads with odd head index give their shared y/z
+                        # rows to the previous head (chain-free by construction)
+                        pg = []
+                        for idx, p in enumerate(heads):
+                            x, y, zz = (int(v) for v in cg[p])
+                            if idx & 1:
+                                q = heads[idx - 1]
+                                dx, dy, dz = (int(cg[p][a]) - int(cg[q][a]) for a in range(3))
+                                if dx == 0 and (dy or dz) and abs(dy) <= 1 and abs(dz) <= 1 and \
+                                        0 <= j + dy <= 1 and 0 <= k + dz <= 1:
+                                    continue
+                            hy = np.uint32((y + j) * int(PY) & 0xffffffff)
+                            hz = np.uint32((zz + k) * int(PZ) & 0xffffffff)
+                            for xi in (0, 1):
+                                e = int((np.uint32(x + xi) ^ hy ^ hz) & mask)
+                                for f in (0, 1):
+                                    pg.append((row0 + e) * 2 + f)
+                        tot["parity_give_yz"] += instr_cost(pg)[0] if pg else 0
                         a1, dd = instr_cost(cur)
                         a2, _ = instr_cost(xm)
                         tot["current"] += a1
