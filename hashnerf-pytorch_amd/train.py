@@ -19,13 +19,14 @@ import math
 import types
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import functional as HF
 from .create import create_nerf
 from .loss import draw_tv_cubes, tv_loss_levels
-from .rays import bbox_for_blender, blender_cameras, blender_intrinsics
+from .rays import bbox_for_blender, blender_cameras, blender_intrinsics, get_rays, pose_spherical
 from .render import img2mse, mse2psnr, render, render_ray_batch
 
 
@@ -74,20 +75,90 @@ def default_args(**over):
     return types.SimpleNamespace(**a)
 
 
-class SyntheticBlender:
-    """Synthetic nerf-synthetic-shaped dataset held in HBM: 100 training
-    cameras on the hemisphere (half-res 400x400, camera_angle_x of chair),
-    bbox from bbox.py's rule, targets uniform in [0,1]^3."""
+def _box_sdf(p, c, h):
+    q = (p - p.new_tensor(c)).abs() - p.new_tensor(h)
+    return q.clamp(min=0).norm(dim=-1) + q.max(-1).values.clamp(max=0)
 
-    def __init__(self, H, W, n, device, seed=0):
+
+# (centre, half extent, albedo) of the procedural chair: seat, back, 4 legs
+_CHAIR_BOXES = (((0., 0., 0.), (.55, .55, .07), (.80, .45, .20)),
+                ((0., -.50, .55), (.55, .06, .48), (.70, .35, .15)),
+                ((.45, .45, -.52), (.06, .06, .45), (.25, .25, .30)),
+                ((-.45, .45, -.52), (.06, .06, .45), (.25, .25, .30)),
+                ((.45, -.45, -.52), (.06, .06, .45), (.25, .25, .30)),
+                ((-.45, -.45, -.52), (.06, .06, .45), (.25, .25, .30)))
+_CHAIR_BALL = ((.15, .10, .30), .22, (.20, .45, .85))
+
+
+def procedural_field(pts):
+    """Analytic chair-like radiance field (density from a sharpened box/sphere
+    SDF union, albedo with a sinusoidal texture): pts [..., 3] -> sigma [...],
+    rgb [..., 3].  The stand-in for nerf-synthetic's chair, which is not in
+    the image: a scene the hash grid can learn, so PSNR curves mean something."""
+    sdfs = [_box_sdf(pts, c, h) for c, h, _ in _CHAIR_BOXES]
+    sdfs.append((pts - pts.new_tensor(_CHAIR_BALL[0])).norm(dim=-1) - _CHAIR_BALL[1])
+    sdf = torch.stack(sdfs, -1)
+    d, k = sdf.min(-1)
+    albedo = pts.new_tensor([a for _, _, a in _CHAIR_BOXES] + [_CHAIR_BALL[2]])[k]
+    s = lambda k: torch.sin(k * pts[..., 0]) * torch.sin(k * pts[..., 1]) * torch.sin(k * pts[..., 2])
+    # a coarse pattern plus grain finer than a finest-level voxel and than a
+    # pixel at 200x200 (period 0.0086 vs 0.016 / 0.014)
+    tex = 0.65 + 0.15 * s(14.) + 0.2 * s(733.)
+    sigma = 60. * torch.sigmoid(-60. * d)
+    return sigma, (albedo * tex[..., None]).clamp(0., 1.)
+
+
+@torch.no_grad()
+def render_procedural(H, W, K, c2w, near=2., far=6., n_samples=384, chunk=8192, white_bkgd=True):
+    """Ground-truth image [H, W, 3] of procedural_field by dense midpoint
+    quadrature of the volume-rendering integral (alpha compositing as
+    raw2outputs, white background as blender)."""
+    ro, rd = get_rays(H, W, K, c2w[:3, :4])
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    t = near + (far - near) * (torch.arange(n_samples, device=ro.device) + .5) / n_samples
+    delta = (far - near) / n_samples
+    out = []
+    for i in range(0, ro.shape[0], chunk):
+        o, d = ro[i:i + chunk], rd[i:i + chunk]
+        pts = o[:, None] + d[:, None] * t[None, :, None]
+        sigma, rgb = procedural_field(pts)
+        alpha = 1. - torch.exp(-sigma * delta * d.norm(dim=-1, keepdim=True))
+        trans = torch.cumprod(torch.cat([torch.ones_like(alpha[:, :1]), 1. - alpha + 1e-10], -1), -1)[:, :-1]
+        w = alpha * trans
+        c = (w[..., None] * rgb).sum(1)
+        if white_bkgd:
+            c = c + (1. - w.sum(-1, keepdim=True))
+        out.append(c)
+    return torch.cat(out, 0).reshape(H, W, 3)
+
+
+class SyntheticBlender:
+    """Synthetic nerf-synthetic-shaped dataset held in HBM: n training
+    cameras on the hemisphere (camera_angle_x of chair), bbox from bbox.py's
+    rule.  scene="uniform": targets uniform in [0,1]^3 (speed runs);
+    scene="procedural": images of procedural_field rendered on the device
+    (PSNR runs), plus n_test held-out views (test_poses, test_images)."""
+
+    def __init__(self, H, W, n, device, seed=0, scene="uniform", n_test=0):
         self.H, self.W = H, W
         self.focal, self.K = blender_intrinsics(H, W)
         poses = blender_cameras(n)
         self.poses = torch.stack(poses, 0).to(device)
         self.bounding_box = bbox_for_blender(poses, H, W, self.focal)
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        self.images = torch.rand((n, H, W, 3), generator=g).to(device)
+        if scene == "uniform":
+            g = torch.Generator(device="cpu").manual_seed(seed)
+            self.images = torch.rand((n, H, W, 3), generator=g).to(device)
+        elif scene == "procedural":
+            self.images = torch.stack([render_procedural(H, W, self.K, c) for c in self.poses], 0)
+        else:
+            raise ValueError(f"SyntheticBlender scene {scene!r}")
         self.i_train = torch.arange(n)
+        # held-out views between the training azimuths, elevation -45
+        th = np.linspace(-180, 180, n_test + 1)[:-1] + 180. / max(n, 1)
+        self.test_poses = torch.stack([pose_spherical(float(t), -45., 4.0) for t in th], 0).to(device) \
+            if n_test else None
+        self.test_images = torch.stack([render_procedural(H, W, self.K, c) for c in self.test_poses], 0) \
+            if (n_test and scene == "procedural") else None
 
 
 def _step_seed(seed, rank, step):
@@ -189,10 +260,14 @@ class Trainer:
         self._one = torch.ones((), device=self.device)
         self._grads = True
 
-    def _fused_forward_backward(self, i: int):
+    def draw_batch(self, i: int):
+        """The random inputs of step i, drawn the way run_nerf.py:576-605 and
+        render_rays draw them: the image (host generator), N_rand pixels
+        without replacement (device sampler, centre crop before
+        precrop_iters), the stratified jitter t_rand and importance uniforms u
+        (device RNG), and the TV cubes + min vertices (rank 0, i <= tv_until).
+        Returns a dict rays [B, 11], target [B, 3], t_rand, u, tv (or None)."""
         a, d, kw = self.args, self.data, self.kw_train
-        if self._grads is None:
-            self._fused_setup()
         B = a.N_rand
         img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
         crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
@@ -202,12 +277,24 @@ class Trainer:
         t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
         u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
              torch.linspace(0., 1., kw["N_importance"], device=self.device).expand(B, kw["N_importance"]))
+        tv = None
+        if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
+            tv = draw_tv_cubes(self.embed_fn.n_levels, self.embed_fn.base_resolution,
+                               self.embed_fn.finest_resolution, self.cpu_gen)
+        return dict(rays=rays, target=target, t_rand=t_rand, u=u, tv=tv)
+
+    def _fused_forward_backward(self, i: int, batch=None):
+        a = self.args
+        if self._grads is None:
+            self._fused_setup()
+        if batch is None:
+            batch = self.draw_batch(i)
+        rays, target, t_rand, u = batch["rays"], batch["target"], batch["t_rand"], batch["u"]
         table = self.embed_fn.table
         out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
         tv = mv = cubes = None
-        if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
-            cubes, mv0 = draw_tv_cubes(self.embed_fn.n_levels, self.embed_fn.base_resolution,
-                                       self.embed_fn.finest_resolution, self.cpu_gen)
+        if batch["tv"] is not None:
+            cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
         lo = HF.loss_fwd(out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts)
@@ -224,10 +311,14 @@ class Trainer:
             p.grad = g
         return lo[0], lo[1]
 
-    def step(self, i: int):
+    def step(self, i: int, batch=None):
+        """One iteration; ``batch`` (explicit mode) = draw_batch(i) drawn by
+        the caller, e.g. to feed the same inputs to a reference path."""
         a = self.args
+        if batch is not None and self.mode != "explicit":
+            raise ValueError("Trainer.step(batch=...) needs mode='explicit'")
         if self.mode == "explicit":
-            loss, mse = self._fused_forward_backward(i)
+            loss, mse = self._fused_forward_backward(i, batch)
         else:
             self.optimizer.zero_grad(set_to_none=True)
             if self.mode == "autograd":

@@ -1,0 +1,177 @@
+"""PSNR parity at equal iterations (BASELINE metric "PSNR@5k iters"; SURVEY
+8(d): "PSNR within +-0.1 of reference at equal iterations").
+
+nerf-synthetic is not in the image, so both runs train on a procedural chair
+(``train.procedural_field``: box/sphere SDF density, textured albedo) whose
+views are rendered on the device by dense quadrature.  Two trainings start
+from the SAME initial parameters and consume the SAME inputs every step (one
+``Trainer.draw_batch`` per step: image, pixels, jitter, importance uniforms,
+TV cubes):
+
+* HIP path: ``Trainer`` (explicit mode) -- fused render fwd/bwd, fused loss,
+  TV, RAdam kernel, the lr decay of run_nerf.py:647-651;
+* reference path: the oracle (our pinned restatement of run_nerf_helpers /
+  hash_encoding / loss / radam) evaluated with eager torch ops --
+  on the GPU, because 5k reference iterations on the host would take a day;
+  its numbers are still those of the reference's algorithm, pinned on the CPU
+  by tests/test_oracle_golden.py.
+
+Both are then evaluated on held-out views (deterministic sampling, the test
+kwargs of create_nerf) with the reference's per-image PSNR averaged
+(run_nerf_helpers.py:430-455).  The trajectories are not bit-identical (MFMA
+vs BLAS summation order, atomic order), so the check is the statistical one
+the metric states: |PSNR_hip - PSNR_ref| <= 0.1 dB at 5k iterations (0.25 dB
+for the short default run, whose PSNR still climbs steeply), PSNR being the
+median over the evaluations in the last 20 % of the run (one evaluation
+swings with the optimizer's step noise).  HN_PSNR_SEEDS=k adds k HIP-only runs
+at other seeds, to show how far two equally good runs land apart.
+
+The default run is short (HN_PSNR_ITERS, default 400 iterations at 100x100,
+50 views); HN_PSNR_ITERS=5000 HN_PSNR_EVERY=100 HN_PSNR_RES=200
+HN_PSNR_NTRAIN=100 HN_PSNR_OUT=path gives the "@5k" figure and writes the
+curve as JSON (profiles/r01/psnr_5k.json).
+"""
+import json
+import math
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL_DB = 0.1          # at 5k iterations (the metric's bar)
+TOL_DB_SHORT = 0.25   # short runs: PSNR still climbs ~1 dB / 100 it, 0.4 dB swings seen mid-run
+
+
+def _oracle_trainer(O, tr, dev):
+    """Reference-path state initialised from the HIP trainer's parameters."""
+    tab = tr.embed_fn.table.detach().clone().requires_grad_(True)
+    wc = {k: w.detach().clone().requires_grad_(True)
+          for k, w in zip(O.MLP_KEYS, tr.kw_train["network_fn"].weights())}
+    wf = {k: w.detach().clone().requires_grad_(True)
+          for k, w in zip(O.MLP_KEYS, tr.kw_train["network_fine"].weights())}
+    params = [(tab, 0.0, 1e-15)] + [(p, 1e-6, 1e-8) for p in list(wc.values()) + list(wf.values())]
+    state = [(torch.zeros_like(p), torch.zeros_like(p)) for p, _, _ in params]
+    return tab, wc, wf, params, state
+
+
+def _oracle_step(O, ref, i, batch, args, box, res, T, lr):
+    """run_nerf.py:608-651 on the oracle: render_rays + loss (+ TV while
+    i <= tv_until) + backward + RAdam (radam.py:58-92)."""
+    tab, wc, wf, params, state = ref
+    ret = O.render_rays(batch["rays"], wc, wf, tab, box[0], box[1], res, T,
+                        t_rand=batch["t_rand"], u=batch["u"], white_bkgd=True)
+    loss = O.training_loss(ret, batch["target"], args.sparse_loss_weight)
+    if batch["tv"] is not None:
+        _, mv = batch["tv"]
+        tv = sum(O.total_variation_loss(tab[l], l, mv[l], T, finest_res=args.finest_res)
+                 for l in range(16))
+        loss = loss + args.tv_loss_weight * tv
+    for p, _, _ in params:
+        p.grad = None
+    loss.backward()
+    with torch.no_grad():
+        for (p, wd, eps), (m, v) in zip(params, state):
+            O.radam_step(p, p.grad, m, v, i + 1, lr, weight_decay=wd, eps=eps)
+    return float(torch.mean((ret["rgb_map"].detach() - batch["target"]) ** 2))
+
+
+@torch.no_grad()
+def _eval_oracle(O, ref, data, box, res, T, chunk=4096):
+    tab, wc, wf, _, _ = ref
+    psnrs = []
+    for c2w, gt in zip(data.test_poses, data.test_images):
+        ro, rd = O.get_rays(data.H, data.W, data.K, c2w[:3, :4].cpu())
+        ro, rd = ro.reshape(-1, 3).to(DEV), rd.reshape(-1, 3).to(DEV)
+        vd = rd / torch.norm(rd, dim=-1, keepdim=True)
+        rb = torch.cat([ro, rd, 2. * torch.ones_like(rd[:, :1]), 6. * torch.ones_like(rd[:, :1]), vd], -1)
+        rgb = torch.cat([O.render_rays(rb[k:k + chunk], wc, wf, tab, box[0], box[1], res, T,
+                                       white_bkgd=True)["rgb_map"] for k in range(0, rb.shape[0], chunk)])
+        psnrs.append(-10. * math.log10(float(torch.mean((rgb.reshape(gt.shape) - gt) ** 2))))
+    return float(np.mean(psnrs)), psnrs
+
+
+@torch.no_grad()
+def _eval_hip(hn, tr, data):
+    hwf = (data.H, data.W, data.focal)
+    kw = dict(tr.kw_test, near=2., far=6.)
+    hn.render_path(data.test_poses, hwf, data.K, 4096, kw, gt_imgs=data.test_images)
+    ps = list(hn.render_path.last_psnrs)
+    return float(np.mean(ps)), ps
+
+
+def test_psnr_parity_equal_iterations(hn, oracle):
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    O = oracle
+    iters = int(os.environ.get("HN_PSNR_ITERS", "400"))
+    every = int(os.environ.get("HN_PSNR_EVERY", str(max(iters // 8, 1))))
+    H = W = int(os.environ.get("HN_PSNR_RES", "100"))
+    n_train = int(os.environ.get("HN_PSNR_NTRAIN", "50"))
+    args = default_args(N_rand=1024, H=H, W=W, n_train=n_train)
+    data = SyntheticBlender(H, W, n_train, DEV, scene="procedural", n_test=4)
+    tr = Trainer(args, data, DEV, seed=0)
+    box = tuple(torch.as_tensor(t, dtype=torch.float32).to(DEV) for t in data.bounding_box)
+    res = O.level_resolutions(16, 16, args.finest_res)
+    T = args.log2_hashmap_size
+    ref = _oracle_trainer(O, tr, DEV)
+    curve = []
+    t_hip = t_ref = 0.0
+    lr = args.lrate
+    for i in range(iters):
+        batch = tr.draw_batch(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr.step(i, batch)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        _oracle_step(O, ref, i, batch, args, box, res, T, lr)
+        torch.cuda.synchronize()
+        t_hip += t1 - t0
+        t_ref += time.perf_counter() - t1
+        lr = args.lrate * (0.1 ** (i / (args.lrate_decay * 1000)))     # run_nerf.py:647-651
+        assert abs(lr - tr.optimizer.param_groups[0]["lr"]) <= 1e-12 * max(lr, 1.0)
+        if ((i + 1) % every == 0 and ((i + 1) > 0.8 * iters or (i + 1) % (5 * every) == 0)) \
+                or i + 1 == iters:
+            ph, _ = _eval_hip(hn, tr, data)
+            pr, _ = _eval_oracle(O, ref, data, box, res, T)
+            curve.append(dict(iter=i + 1, psnr_hip=round(ph, 4), psnr_ref=round(pr, 4),
+                              diff=round(ph - pr, 4)))
+            print(f"iter {i + 1}: PSNR hip {ph:.3f}  ref {pr:.3f}  diff {ph - pr:+.3f}", flush=True)
+    # the statistic: median PSNR over the evaluations in the last 20 % of the
+    # run (a single evaluation swings with the optimizer's step noise)
+    tail = [c for c in curve if c["iter"] > 0.8 * iters] or curve[-1:]
+    med = lambda k: round(float(np.median([c[k] for c in tail])), 4)
+    mean = lambda k: round(float(np.mean([c[k] for c in tail])), 4)
+    stat = dict(psnr_hip=med("psnr_hip"), psnr_ref=med("psnr_ref"), n_evals=len(tail),
+                from_iter=tail[0]["iter"], mean_hip=mean("psnr_hip"), mean_ref=mean("psnr_ref"))
+    stat["diff"] = round(stat["psnr_hip"] - stat["psnr_ref"], 4)
+    # scale of the bar: the HIP path alone at other seeds (other images,
+    # pixels, jitter and init) -- how far two equally good runs land apart
+    seeds = int(os.environ.get("HN_PSNR_SEEDS", "0"))
+    spread = []
+    for sd in range(1, seeds + 1):
+        t2 = Trainer(args, data, DEV, seed=sd)
+        ps = []
+        for i in range(iters):
+            t2.step(i)
+            if (i + 1) % every == 0 and (i + 1) > 0.8 * iters:
+                ps.append(_eval_hip(hn, t2, data)[0])
+        spread.append(round(float(np.median(ps)), 4))
+    if spread:
+        stat["hip_other_seeds"] = spread
+    tol = TOL_DB if iters >= 5000 else TOL_DB_SHORT
+    out = dict(iters=iters, H=H, W=W, N_rand=args.N_rand, n_train=n_train, n_test=4,
+               scene="procedural chair (train.procedural_field)", tol_db=tol, final=stat, curve=curve,
+               ms_per_iter_hip=round(1e3 * t_hip / iters, 3),
+               ms_per_iter_ref_eager_gpu=round(1e3 * t_ref / iters, 3))
+    print(json.dumps(out["final"]), flush=True)
+    path = os.environ.get("HN_PSNR_OUT")
+    if path:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    assert stat["psnr_hip"] > 12.0, "the HIP path did not learn the scene"
+    assert abs(stat["diff"]) <= tol, out
