@@ -314,3 +314,77 @@ def test_render_image_from_c2w_vs_reference(hn):
     assert rgbs.shape == (2, H, W, 3) and depths.shape == (2, H, W)
     np.testing.assert_allclose(rgbs[0], rgb.cpu().numpy(), rtol=0, atol=0)
     np.testing.assert_allclose(depths[1], ((depth - 2.) / 4.).cpu().numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("box", [((-1.0, -1.0, -1.0), (1.0, 1.0, 1.0)),
+                                 ((-0.6, -1.3, -0.2), (0.9, 0.4, 1.1))])
+def test_fused_step_bbox_tighter_than_samples(hn, oracle, box):
+    """BASELINE configs[4] semantics (scannet: mesh bounds as the bbox,
+    load/load_scannet.py:105; samples range far outside it) -- SURVEY 8a
+    trap 3: out-of-box points use the CLAMPED point's voxel but weights from
+    the UN-clamped point (extrapolated, |w| >> 1), and keep_mask stays
+    all-True.  Fused fwd+bwd against the CPU oracle on the device's own
+    importance samples, sparsity weight raised to 1e-3 so its gradient
+    counts."""
+    from importlib import import_module
+    HF = import_module("hashnerf_pytorch_amd.functional")
+    O = oracle
+    torch.manual_seed(3)
+    B, T, sparse_w = 64, 14, 1e-3
+    bmin, bmax = torch.tensor(box[0]), torch.tensor(box[1])
+    emb = hn.HashEmbedder((bmin, bmax), log2_hashmap_size=T, finest_resolution=512).to(DEV)
+    with torch.no_grad():
+        emb.table.uniform_(-0.3, 0.3)
+    kw = dict(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3, hidden_dim_color=64,
+              input_ch=32, input_ch_views=16)
+    mc, mf = hn.NeRFSmall(**kw).to(DEV), hn.NeRFSmall(**kw).to(DEV)
+    focal, K = hn.rays.blender_intrinsics(64, 64)
+    ro, rd = hn.get_rays(64, 64, K, hn.pose_spherical(40.0, -35.0, 4.0)[:3, :4].to(DEV))
+    sel = torch.randperm(64 * 64, device=DEV)[:B]
+    rays_o, rays_d = ro.reshape(-1, 3)[sel].contiguous(), rd.reshape(-1, 3)[sel].contiguous()
+    # most samples of z in [2, 6] from radius 4 leave this box
+    z = torch.linspace(2., 6., 64, device=DEV)
+    pts = rays_o[:, None] + rays_d[:, None] * z[None, :, None]
+    outside = ((pts < bmin.to(DEV)) | (pts > bmax.to(DEV))).any(-1).float().mean().item()
+    assert outside > 0.5, outside
+    HF.DEBUG_KEEP = True
+    try:
+        rgb, depth, acc, ex = hn.render(64, 64, K, rays=torch.stack([rays_o, rays_d], 0), retraw=True,
+                                        network_query_fn=hn.NetworkQuery(emb, hn.SHEncoder()), perturb=1.,
+                                        N_importance=128, network_fine=mf, N_samples=64, network_fn=mc,
+                                        embed_fn=emb, use_viewdirs=True, white_bkgd=False, ndc=False,
+                                        near=2., far=6., pytest=True)
+    finally:
+        HF.DEBUG_KEEP = False
+    z_fine = HF.LAST["z_fine"].cpu()
+    target = torch.rand(B, 3, generator=torch.Generator().manual_seed(5)).to(DEV)
+    loss, _ = hn.training_loss(rgb, ex, target, sparse_w)
+    loss.backward()
+    rc, rdc = rays_o.cpu(), rays_d.cpu()
+    vd = rdc / torch.norm(rdc, dim=-1, keepdim=True)
+    rb = torch.cat([rc, rdc, 2. * torch.ones(B, 1), 6. * torch.ones(B, 1), vd], -1)
+    np.random.seed(0)
+    t_rand = torch.tensor(np.random.rand(B, 64), dtype=torch.float32)
+    np.random.seed(0)
+    u = torch.tensor(np.random.rand(B, 128), dtype=torch.float32)
+    tab = emb.table.detach().cpu().clone().requires_grad_(True)
+    wc = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in zip(O.MLP_KEYS, mc.weights())}
+    wf = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in zip(O.MLP_KEYS, mf.weights())}
+    ret = O.render_rays(rb, wc, wf, tab, bmin, bmax, O.level_resolutions(16, 16, 512), T,
+                        t_rand=t_rand, u=u, white_bkgd=False, z_fine=z_fine)
+    same = np.isclose(z_fine.numpy(), ret["z_vals"].detach().numpy(), rtol=0, atol=1e-5)
+    assert same.mean() > 0.97, f"only {same.mean():.4f} of fine samples agree"
+    for k, a in (("rgb_map", rgb), ("acc_map", acc), ("sparsity_loss", ex["sparsity_loss"]),
+                 ("rgb0", ex["rgb0"]), ("acc0", ex["acc0"]), ("sparsity_loss0", ex["sparsity_loss0"])):
+        close(a, ret[k].detach().numpy(), rtol=1e-4, atol=2e-5, msg=k)
+    # extrapolated features reach |f| ~ 1e2-1e4, so MLP sums cancel: an
+    # element's summation-order error scales with the tensor's magnitude
+    raw_ref = ret["raw"].detach().numpy()
+    close(ex["raw"], raw_ref, rtol=1e-4, atol=1e-5 * np.abs(raw_ref).max(), msg="raw")
+    ref_loss = O.training_loss(ret, target.cpu(), sparse_w)
+    close(loss.item(), ref_loss.item(), rtol=1e-5, msg="loss")
+    ref_loss.backward()
+    rel_close(emb.table.grad, tab.grad.numpy(), 5e-4, "table grad")
+    for w_dev, w_ref in ((mc.weights(), wc), (mf.weights(), wf)):
+        for p, k in zip(w_dev, O.MLP_KEYS):
+            rel_close(p.grad, w_ref[k].grad.numpy(), 5e-4, k)
