@@ -33,6 +33,13 @@ CONFIGS = {
             N_rand=8192, log2_hashmap_size=22, finest_res=1024, tv_loss_weight=1e-6),
     4: dict(workload="hotdog DP, N_rand=8192 per GPU (BASELINE configs[3])",
             N_rand=8192, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6),
+    # scannet_scene0000.txt: white_bkgd False; the bbox is the mesh bounds
+    # (load/load_scannet.py:105), far tighter than the sample range, so most
+    # samples are out of the box (extrapolated weights, SURVEY trap 3)
+    5: dict(workload="scannet-style unbounded scene: bbox +-1 inside the 2..6 sample range, black bkgd, "
+                     "sparse_loss_weight 1e-3, N_rand=4096 per GPU, 64+128 (BASELINE configs[4])",
+            N_rand=4096, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6,
+            white_bkgd=False, sparse_loss_weight=1e-3, bbox=((-1., -1., -1.), (1., 1., 1.))),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 PT_BYTES = 16 * 8 * 8          # one point: 16 levels x 8 corners x (2 x fp32)
@@ -119,7 +126,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=None)
+    ap.add_argument("--config", type=int, default=None, choices=sorted(CONFIGS))
     ap.add_argument("--n-rand", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -153,8 +160,11 @@ def main():
 
     targs = default_args(N_rand=cfg["N_rand"], log2_hashmap_size=cfg["log2_hashmap_size"],
                          finest_res=cfg["finest_res"], tv_loss_weight=cfg["tv_loss_weight"],
-                         tv_until=10 ** 9)
+                         tv_until=10 ** 9, white_bkgd=cfg.get("white_bkgd", True),
+                         sparse_loss_weight=cfg.get("sparse_loss_weight", 1e-10))
     data = SyntheticBlender(400, 400, 100, dev, seed=0)
+    if "bbox" in cfg:
+        data.bounding_box = tuple(torch.tensor(v) for v in cfg["bbox"])
     tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0)
 
     for i in range(args.warmup):
