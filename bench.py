@@ -51,13 +51,13 @@ FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
 BWD_KERNELS = ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel")   # hn_render_bwd
 
 
-def measured_traffic(cfg_id, n_rand_override):
+def measured_traffic(cfg_id, n_rand_override, scene, pretrain):
     """HBM-side bytes per hn_render_bwd launch from the last PMC passes of the
-    same workload (scripts/gpu_pmc.sh -> profiles/traffic_config<N>.json):
+    same workload (scripts/gpu_pmc.sh -> profiles/traffic_config<N>_<scene>_p<pretrain>.json):
     2 x FETCH_SIZE + WRITE_SIZE summed over the launch's kernels.  PMC
     counters need their own rocprofv3 passes, so bench.py cannot collect
     them live; None when no file matches this workload."""
-    path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}.json")
+    path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}_{scene}_p{pretrain}.json")
     if n_rand_override or not os.path.exists(path):
         return None, None, None
     t = json.load(open(path))
@@ -129,6 +129,14 @@ def main():
     ap.add_argument("--config", type=int, default=None, choices=sorted(CONFIGS))
     ap.add_argument("--n-rand", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # the default workload is the chair stand-in in its trained regime: 1000
+    # untimed steps first (~2 s), so the timed steps see the sample
+    # distribution of most of a 5k-iteration run rather than of the first
+    # precrop steps of an untrained network
+    ap.add_argument("--scene", default="procedural", choices=("uniform", "procedural"),
+                    help="uniform: random targets; procedural: train.procedural_field chair images")
+    ap.add_argument("--pretrain", type=int, default=1000,
+                    help="untimed training steps before warmup")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
@@ -162,12 +170,14 @@ def main():
                          finest_res=cfg["finest_res"], tv_loss_weight=cfg["tv_loss_weight"],
                          tv_until=10 ** 9, white_bkgd=cfg.get("white_bkgd", True),
                          sparse_loss_weight=cfg.get("sparse_loss_weight", 1e-10))
-    data = SyntheticBlender(400, 400, 100, dev, seed=0)
+    t_data = time.perf_counter()
+    data = SyntheticBlender(400, 400, 100, dev, seed=0, scene=args.scene)
+    t_data = time.perf_counter() - t_data
     if "bbox" in cfg:
         data.bounding_box = tuple(torch.tensor(v) for v in cfg["bbox"])
     tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0)
 
-    for i in range(args.warmup):
+    for i in range(args.pretrain + args.warmup):
         tr.step(i)
     torch.cuda.synchronize()
     if world > 1:
@@ -176,7 +186,8 @@ def main():
     HF.TIMER.reset()
     HF.TIMER.enabled = True
     t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
+    i0 = args.pretrain + args.warmup
+    for i in range(i0, i0 + args.steps):
         loss, mse = tr.step(i)
     torch.cuda.synchronize()
     if world > 1:
@@ -193,7 +204,7 @@ def main():
     B = cfg["N_rand"]
     value = world * B * args.steps / dt
     if rank == 0:
-        traffic, traffic_src, atomics = measured_traffic(cfg_id, args.n_rand)
+        traffic, traffic_src, atomics = measured_traffic(cfg_id, args.n_rand, args.scene, args.pretrain)
         bwd_gbs = B * BWD_BYTES_PER_RAY / (bwd_ms * 1e-3) / 1e9
         fwd_gbs = B * FWD_BYTES_PER_RAY / (fwd_ms * 1e-3) / 1e9
         line = {
@@ -201,7 +212,10 @@ def main():
             "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (procedural 400x400 blender-style cameras, uniform targets)",
+            "data": ("synthetic: 100 blender-style 400x400 cameras, " +
+                     ("uniform random targets" if args.scene == "uniform" else
+                      f"procedural chair images (train.procedural_field, rendered in {t_data:.1f} s)") +
+                     (f", timed after {args.pretrain} untimed training steps" if args.pretrain else "")),
             "config": {"workload": cfg["workload"], "rays_per_gpu": B, "global_batch": B * world,
                        "samples_per_ray": "64+128", "log2_hashmap_size": cfg["log2_hashmap_size"],
                        "finest_res": cfg["finest_res"], "parallelism": f"dp{world}"},

@@ -19,5 +19,10 @@ timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 > $OUT/bench_$TAG.js
 cat $OUT/bench_$TAG.json && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o prof -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
-echo "chain rc=$?"
+RC=$?
+# the timed steps only (the 13 last dispatches of each kernel: 3 warmup + 10 timed)
+[ $RC -eq 0 ] && python3 scripts/trace_tail_stats.py $OUT/prof_$TAG/prof_kernel_trace.csv 10 \
+    > $OUT/prof_$TAG/prof_kernel_stats_timed.csv
+rm -f $OUT/prof_$TAG/prof_kernel_trace.csv   # per-dispatch rows of the pretraining too: large
+echo "chain rc=$RC"
 tail -3 $OUT/smoke_$TAG.log

@@ -27,16 +27,29 @@ for P in "${PASSES[@]}"; do
       || { echo "pass $i ($P) failed: $(tail -2 $OUT/pmc_${TAG}_$i.log)"; exit 1; }
 done
 python3 - "$OUT" "$TAG" "$*" <<'EOF' | tee $OUT/pmc_$TAG.txt
-import csv, glob, json, sys, collections
+import csv, glob, json, os, sys, collections
 out, tag, bench_args = sys.argv[1], sys.argv[2], sys.argv[3]
-agg = collections.defaultdict(lambda: collections.defaultdict(list))
+# only the last PMC_LAST dispatches of each kernel (the timed steps; the
+# bench's untimed pretraining steps come first in dispatch order)
+last = int(os.environ.get("PMC_LAST", "4"))
+raw = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{out}/pmc_{tag}_*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", r.get("Kernel-Name", ""))
         if "hn::" not in name:
             continue
         key = name.split("(")[0].replace("void ", "")
-        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        did = int(r.get("Dispatch_Id", r.get("Dispatch-Id", 0)) or 0)
+        raw[key][r["Counter_Name"]].append((did, float(r["Counter_Value"])))
+agg = collections.defaultdict(dict)
+for k, cs in raw.items():
+    for c, v in cs.items():
+        # several rows per dispatch (per-XCD/SE instances) are summed
+        per = collections.defaultdict(float)
+        for did, x in v:
+            per[did] += x
+        ids = sorted(per)[-last:]
+        agg[k][c] = [per[i] for i in ids]
 for k, cs in sorted(agg.items()):
     print(k)
     for c, v in sorted(cs.items()):
@@ -55,3 +68,6 @@ for k, cs in agg.items():
         traffic["kernels"][k.replace("hn::", "")] = ent
 json.dump(traffic, open(f"{out}/traffic_{tag}.json", "w"), indent=1)
 EOF
+# the raw per-dispatch CSVs (every pretraining dispatch too) are tens of MB:
+# keep only the summaries (gpurun copies back at most 64 MiB)
+rm -rf $OUT/pmc_${TAG}_*/
