@@ -19,7 +19,7 @@ MAX_LEVELS = 32
 ABI_VERSION = 3                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
-MLP_PACKED_FLOATS = 24064
+MLP_PACKED_FLOATS = 30208
 
 _lib = None
 

@@ -269,6 +269,64 @@ HN_DEV f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 HN_DEV constexpr int row_of(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ---------------------------------------------------------------------------
+// Split-f32 products on the bf16 MFMA.  An f32 x is carried as NS bf16 parts
+// x = p0 + p1 (+ p2) + r, p_q = bf16(x - p0 - .. - p_{q-1}) (RNE, each residual
+// exact in f32), |r| <= 2^-18 |x| for NS = 2 and 2^-27 |x| for NS = 3.  The
+// products p_q(a) p_q'(b) are exact in the f32 accumulator; keeping those with
+// q + q' < NS gives a . b to ~2^-17 (NS = 2) or ~2^-25 (NS = 3) relative per
+// product -- NS = 3 is as accurate as one f32 rounding.
+// v_mfma_f32_32x32x16_bf16 contracts K = 16 in 32 cycles per SIMD: NS = 3 is
+// six of them (192 cycles) against eight v_mfma_f32_32x32x2_f32 (512 cycles)
+// for the same K, NS = 2 three (96 cycles).
+//   Operand map (32x32x16 bf16): lane l holds A[row l&31][k = 8(l>>5) + j] and
+//   B[k = 8(l>>5) + j][col l&31] in element j = 0..7; C/D as the f32 form.
+// A K = 16 chunk c of a chained GEMM takes element j of lane half h from the
+// f32 k-step s = 8c + j of the same lane half: the k <-> input-row map is the
+// f32 form's, so packed A fragments and D -> B chaining keep their layout.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+template <int NS>
+struct SP {   // one K = 16 operand chunk as NS bf16 parts, p[0] the largest
+  bf16x8 p[NS];
+};
+template <int NS, typename F>
+HN_DEV SP<NS> splitn(F x) {
+  SP<NS> s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = x(j);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const __bf16 b = (__bf16)v;
+      s.p[q][j] = b;
+      if (q + 1 < NS) v = v - (float)b;
+    }
+  }
+  return s;
+}
+template <int NS>
+HN_DEV SP<NS> splitn(const f32x4 a, const f32x4 b) {
+  return splitn<NS>([&](int j) { return j < 4 ? a[j] : b[j - 4]; });
+}
+HN_DEV bf16x8 as_bf16x8(const f32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+HN_DEV f32x16 mfma_bf(const bf16x8 a, const bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// acc += A . B, both as NS parts; the smallest products first
+template <int NS>
+HN_DEV f32x16 mfma_split(const SP<NS>& a, const SP<NS>& b, f32x16 c) {
+  static_assert(NS == 2 || NS == 3, "parts");
+  if constexpr (NS == 3) {
+    c = mfma_bf(a.p[2], b.p[0], c);
+    c = mfma_bf(a.p[0], b.p[2], c);
+    c = mfma_bf(a.p[1], b.p[1], c);
+  }
+  c = mfma_bf(a.p[1], b.p[0], c);
+  c = mfma_bf(a.p[0], b.p[1], c);
+  return mfma_bf(a.p[0], b.p[0], c);
+}
 // Level handled by register pair (2m, 2m+1) of lane half h in the 32-feature
 // tile layout: feature ROW(2m,h) = 2 * lev(m,h).
 HN_DEV constexpr int tile_level(int m, int h) { return (m & 1) + 4 * (m >> 1) + 2 * h; }

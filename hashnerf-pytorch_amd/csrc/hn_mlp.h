@@ -21,46 +21,89 @@
 
 namespace hn {
 
-// Packed A-operand GEMMs (offsets in floats; size = OB * KS * 64, KS % 4 == 0).
+// Packed A-operand GEMMs ("regions"), per net, in this order.  KS = f32 k-steps
+// (K = 2 each), OB = 32-row output blocks.  A region is OB x groups x 256
+// floats; a group is one 1-KiB dwordx4 load per wave.
+//   f32 region  (NS = 0): group g = the f32 fragments of k-steps 4g .. 4g+3;
+//   split region (NS parts, hn_common.h): chunk c (k-steps 8c .. 8c+7) is NS
+//   groups, group NS*c + q = part q of those 8 values as bf16 (dword d of a
+//   lane = elements 2d, 2d+1).
+// HN_SPLIT_F: parts in the forward GEMMs (the forward pass and the backward's
+// recompute, which therefore reproduce each other's activations bit for bit);
+// 3 makes them as accurate as f32.  HN_SPLIT_B: parts in the data-gradient and
+// weight-gradient GEMMs.  0 = f32 MFMA (an exact FMA chain).  color_net.2^T
+// (4 k-steps, 2 used) is always f32.
+#ifndef HN_SPLIT_F
+#define HN_SPLIT_F 3
+#endif
+#ifndef HN_SPLIT_B
+#define HN_SPLIT_B 2
+#endif
+#ifndef HN_SPLIT_W   // parts in the fused backward's weight-gradient products
+#define HN_SPLIT_W HN_SPLIT_B
+#endif
+enum : int { R_F0, R_F1, R_F2G, R_F2S, R_F3, R_F4, R_B4, R_B3, R_B2G, R_B2S, R_B1, R_B0, R_N };
+//  F0 sigma_net.0  F1 sigma_net.1  F2G/F2S color_net.0 geo/sh  F3 color_net.1  F4 color_net.2
+//  B4 color_net.2^T  B3 color_net.1^T  B2G/B2S color_net.0^T geo/sh  B1 sigma_net.1^T  B0 sigma_net.0^T
+constexpr int kRegKS[R_N] = {16, 32, 8, 8, 32, 32, 4, 32, 32, 32, 8, 32};
+constexpr int kRegOB[R_N] = {2, 1, 2, 2, 2, 1, 2, 2, 1, 1, 2, 1};
+constexpr int reg_ns(int r) { return kRegKS[r] % 8 ? 0 : (r < R_B4 ? HN_SPLIT_F : HN_SPLIT_B); }
+constexpr int reg_gpo(int r) { return reg_ns(r) ? reg_ns(r) * kRegKS[r] / 8 : kRegKS[r] / 4; }   // groups per OB
+constexpr int reg_off(int r) {
+  int o = 0;
+  for (int i = 0; i < r; ++i) o += kRegOB[i] * reg_gpo(i) * 256;
+  return o;
+}
 enum : int {
-  G_F0 = 0,        // sigma_net.0        OB 2  KS 16
-  G_F1 = 2048,     // sigma_net.1        OB 1  KS 32
-  G_F2G = 4096,    // color_net.0 geo    OB 2  KS 8
-  G_F2S = 5120,    // color_net.0 sh     OB 2  KS 8
-  G_F3 = 6144,     // color_net.1        OB 2  KS 32
-  G_F4 = 10240,    // color_net.2        OB 1  KS 32
-  G_B4 = 12288,    // color_net.2^T      OB 2  KS 4 (2 used)
-  G_B3 = 12800,    // color_net.1^T      OB 2  KS 32
-  G_B2G = 16896,   // color_net.0^T geo  OB 1  KS 32
-  G_B2S = 18944,   // color_net.0^T sh   OB 1  KS 32
-  G_B1 = 20992,    // sigma_net.1^T      OB 2  KS 8
-  G_B0 = 22016,    // sigma_net.0^T      OB 1  KS 32
-  G_END = 24064
+  G_F0 = reg_off(R_F0), G_F1 = reg_off(R_F1), G_F2G = reg_off(R_F2G), G_F2S = reg_off(R_F2S),
+  G_F3 = reg_off(R_F3), G_F4 = reg_off(R_F4), G_B4 = reg_off(R_B4), G_B3 = reg_off(R_B3),
+  G_B2G = reg_off(R_B2G), G_B2S = reg_off(R_B2S), G_B1 = reg_off(R_B1), G_B0 = reg_off(R_B0),
+  G_END = reg_off(R_N)
 };
-static_assert(G_END == HN_MLP_PACKED_FLOATS, "packed size");
+static_assert(G_END <= HN_MLP_PACKED_FLOATS, "packed size");
 
 // Weight-gradient accumulator layout (torch [out][in] row-major, concatenated).
 enum : int { W_S0 = 0, W_S1 = 2048, W_C0 = 3072, W_C1 = 5056, W_C2 = 9152, W_END = 9344 };
 static_assert(W_END == HN_MLP_PARAMS, "param count");
 
-// acc += A(gemm at off, block ob) . B where bval(s) is the B operand of k-step s.
-// The next group's A fragment is loaded while the current group's 4 MFMAs run;
-// the scheduling barrier stops hipcc from hoisting all loads (register blowup).
-template <int KS, typename BF>
-HN_DEV f32x16 gemm(const float* __restrict__ P, int off, int ob, f32x16 acc, int lane, BF bval) {
+// acc += A(region R, block ob) . B where bval(s) is the B operand of f32 k-step s.
+// The next A fragments are loaded while the current ones' MFMAs run; the
+// scheduling barrier stops hipcc from hoisting all loads (register blowup).
+template <int R, typename BF>
+HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF bval) {
+  constexpr int KS = kRegKS[R], NS = reg_ns(R), GPO = reg_gpo(R), OFF = reg_off(R);
   // opaque BEFORE the offset: keeps hipcc from precomputing ~50 uniform GEMM
   // base addresses at the top of the tile loop (SGPR pairs that then spill)
-  const float* base = opaque_ptr(P) + off + ob * (KS / 4) * 256 + lane * 4;
-  f32x4 an = *reinterpret_cast<const f32x4*>(base);
+  const float* base = opaque_ptr(P) + OFF + ob * GPO * 256 + lane * 4;
+  if constexpr (NS > 0) {                       // split-f32 on the bf16 MFMA
+    SP<NS> an;
 #pragma unroll
-  for (int g = 0; g < KS / 4; ++g) {
-    const f32x4 a = an;
-    if (g + 1 < KS / 4) an = *reinterpret_cast<const f32x4*>(base + (g + 1) * 256);
+    for (int q = 0; q < NS; ++q) an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + q * 256));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int c = 0; c < KS / 8; ++c) {
+      const SP<NS> a = an;
+      if (c + 1 < KS / 8) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+          an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + (NS * (c + 1) + q) * 256));
+      }
+      const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
+      acc = mfma_split<NS>(a, b, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+  } else {
+    f32x4 an = *reinterpret_cast<const f32x4*>(base);
+#pragma unroll
+    for (int g = 0; g < KS / 4; ++g) {
+      const f32x4 a = an;
+      if (g + 1 < KS / 4) an = *reinterpret_cast<const f32x4*>(base + (g + 1) * 256);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
   }
-  return acc;
 }
 
 struct MlpAct {
@@ -85,27 +128,27 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   // sigma_net.0: 32 -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    a.h0[ob] = gemm<16>(P, G_F0, ob, zero16(), lane, [&](int s) { return feat[s]; });
+    a.h0[ob] = gemm<R_F0>(P, ob, zero16(), lane, [&](int s) { return feat[s]; });
     relu16(a.h0[ob]);
   }
   // sigma_net.1: 64 -> 16 (sigma, geo15), no activation
-  a.s1 = gemm<32>(P, G_F1, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
+  a.s1 = gemm<R_F1>(P, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
   // color_net.0: [sh16 | geo15] -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    f32x16 acc = gemm<8>(P, G_F2S, ob, zero16(), lane, [&](int s) { return sh8[s]; });
-    acc = gemm<8>(P, G_F2G, ob, acc, lane, [&](int s) { return a.s1[s]; });
+    f32x16 acc = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+    acc = gemm<R_F2G>(P, ob, acc, lane, [&](int s) { return a.s1[s]; });
     relu16(acc);
     a.c0[ob] = acc;
   }
   // color_net.1: 64 -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    a.c1[ob] = gemm<32>(P, G_F3, ob, zero16(), lane, [&](int s) { return a.c0[s >> 4][s & 15]; });
+    a.c1[ob] = gemm<R_F3>(P, ob, zero16(), lane, [&](int s) { return a.c0[s >> 4][s & 15]; });
     relu16(a.c1[ob]);
   }
   // color_net.2: 64 -> 3, no activation
-  c2 = gemm<32>(P, G_F4, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });
+  c2 = gemm<R_F4>(P, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });
 }
 
 // ---------------------------------------------------------------------------
@@ -192,7 +235,7 @@ HN_DEV void mlp_bwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   f32x16 dc1[2];
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    dc1[ob] = gemm<4>(P, G_B4, ob, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+    dc1[ob] = gemm<R_B4>(P, ob, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
     mask16(dc1[ob], a.c1[ob]);
   }
   // ---- color_net.1 ----
@@ -209,7 +252,7 @@ HN_DEV void mlp_bwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   f32x16 dc0[2];
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    dc0[ob] = gemm<32>(P, G_B3, ob, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+    dc0[ob] = gemm<R_B3>(P, ob, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
     mask16(dc0[ob], a.c0[ob]);
   }
   // ---- color_net.0: X = [sh16 | geo15] ----
@@ -225,10 +268,10 @@ HN_DEV void mlp_bwd_tile(const float* __restrict__ P, const f32x16& feat, const 
     stage_tile(Tdy, dc0[nb], lane);
     wgrad_accum(Tdy, Tx, Wacc, W_C0, 31, nb * 32, 64, 0, 31, lane);
   }
-  f32x16 ds1 = gemm<32>(P, G_B2G, 0, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+  f32x16 ds1 = gemm<R_B2G>(P, 0, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
   if (h == 0) ds1[0] = dsig;                    // row 0 = sigma (A row 0 is zero)
   if (dsh != nullptr)
-    *dsh = gemm<32>(P, G_B2S, 0, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+    *dsh = gemm<R_B2S>(P, 0, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
   // ---- sigma_net.1 ----
   stage_tile(Tdy, ds1, lane);
 #pragma unroll
@@ -239,7 +282,7 @@ HN_DEV void mlp_bwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   f32x16 dh0[2];
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    dh0[ob] = gemm<8>(P, G_B1, ob, zero16(), lane, [&](int s) { return ds1[s]; });
+    dh0[ob] = gemm<R_B1>(P, ob, zero16(), lane, [&](int s) { return ds1[s]; });
     mask16(dh0[ob], a.h0[ob]);
   }
   // ---- sigma_net.0 ----
@@ -249,48 +292,52 @@ HN_DEV void mlp_bwd_tile(const float* __restrict__ P, const f32x16& feat, const 
     stage_tile(Tdy, dh0[nb], lane);
     wgrad_accum(Tdy, Tx, Wacc, W_S0, 32, nb * 32, 64, 0, 32, lane);
   }
-  dfeat = gemm<32>(P, G_B0, 0, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  dfeat = gemm<R_B0>(P, 0, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
 }
 
 // Packing: natural torch weights -> fragment-ordered A operands (per net).
-HN_DEV float pack_value(const hn_mlp& w, int idx) {
-  int off, KS;
-  if (idx < G_F1) { off = G_F0; KS = 16; }
-  else if (idx < G_F2G) { off = G_F1; KS = 32; }
-  else if (idx < G_F2S) { off = G_F2G; KS = 8; }
-  else if (idx < G_F3) { off = G_F2S; KS = 8; }
-  else if (idx < G_F4) { off = G_F3; KS = 32; }
-  else if (idx < G_B4) { off = G_F4; KS = 32; }
-  else if (idx < G_B3) { off = G_B4; KS = 4; }
-  else if (idx < G_B2G) { off = G_B3; KS = 32; }
-  else if (idx < G_B2S) { off = G_B2G; KS = 32; }
-  else if (idx < G_B1) { off = G_B2S; KS = 32; }
-  else if (idx < G_B0) { off = G_B1; KS = 8; }
-  else { off = G_B0; KS = 32; }
-  const int rel = idx - off;
-  const int j = rel & 3;
-  const int lane = (rel >> 2) & 63;
-  const int t = rel >> 8;
-  const int g = t % (KS / 4), ob = t / (KS / 4);
-  const int s = 4 * g + j;
+// f32 value of region r's A fragment: out block ob, k-step s, lane.
+HN_DEV float pack_f32(const hn_mlp& w, int r, int ob, int s, int lane) {
   const int i = lane & 31, h = lane >> 5;
   const int o = ob * 32 + i;
   const int kc = 32 * (s >> 4) + row_of(s & 15, h);   // chain order (D-layout input)
   const int kp = 2 * s + h;                            // pair order
-  switch (off) {
-    case G_F0: return w.sigma0[o * 32 + kc];
-    case G_F1: return i < 16 ? w.sigma1[i * 64 + kc] : 0.f;
-    case G_F2G: return (kc >= 1 && kc <= 15) ? w.color0[o * 31 + 15 + kc] : 0.f;
-    case G_F2S: return w.color0[o * 31 + kp];
-    case G_F3: return w.color1[o * 64 + kc];
-    case G_F4: return i < 3 ? w.color2[i * 64 + kc] : 0.f;
-    case G_B4: return kp < 3 ? w.color2[kp * 64 + o] : 0.f;
-    case G_B3: return w.color1[kc * 64 + o];
-    case G_B2G: return (i >= 1 && i <= 15) ? w.color0[kc * 31 + 15 + i] : 0.f;
-    case G_B2S: return i < 16 ? w.color0[kc * 31 + i] : 0.f;
-    case G_B1: return w.sigma1[kc * 64 + o];
-    default: return w.sigma0[kc * 32 + i];   // G_B0
+  switch (r) {
+    case R_F0: return w.sigma0[o * 32 + kc];
+    case R_F1: return i < 16 ? w.sigma1[i * 64 + kc] : 0.f;
+    case R_F2G: return (kc >= 1 && kc <= 15) ? w.color0[o * 31 + 15 + kc] : 0.f;
+    case R_F2S: return w.color0[o * 31 + kp];
+    case R_F3: return w.color1[o * 64 + kc];
+    case R_F4: return i < 3 ? w.color2[i * 64 + kc] : 0.f;
+    case R_B4: return kp < 3 ? w.color2[kp * 64 + o] : 0.f;
+    case R_B3: return w.color1[kc * 64 + o];
+    case R_B2G: return (i >= 1 && i <= 15) ? w.color0[kc * 31 + 15 + i] : 0.f;
+    case R_B2S: return i < 16 ? w.color0[kc * 31 + i] : 0.f;
+    case R_B1: return w.sigma1[kc * 64 + o];
+    default: return w.sigma0[kc * 32 + i];   // R_B0
   }
+}
+
+// Float idx of the packed buffer (layout above).
+HN_DEV float pack_value(const hn_mlp& w, int idx) {
+  int r = 0;
+  while (r + 1 < R_N && idx >= reg_off(r + 1)) ++r;
+  const int rel = idx - reg_off(r), d = rel & 3, lane = (rel >> 2) & 63, t = rel >> 8;
+  const int gpo = reg_gpo(r), ns = reg_ns(r), g = t % gpo, ob = t / gpo;
+  if (ns == 0) return pack_f32(w, r, ob, 4 * g + d, lane);
+  const int c = g / ns, part = g % ns;
+  uint32_t out = 0;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    float v = pack_f32(w, r, ob, 8 * c + 2 * d + e, lane);
+    __bf16 b = (__bf16)v;
+    for (int q = 0; q < part; ++q) {
+      v = v - (float)b;
+      b = (__bf16)v;
+    }
+    out |= (uint32_t)__builtin_bit_cast(uint16_t, b) << (16 * e);
+  }
+  return __uint_as_float(out);
 }
 
 // Launch the packing kernel (hn_mlp.hip).

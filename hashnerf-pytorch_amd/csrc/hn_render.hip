@@ -365,6 +365,17 @@ HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
   const int h = lane >> 5;
   const f32x4* pa = reinterpret_cast<const f32x4*>(X + arow * kXS + 16 * h);
   const f32x4* pb = reinterpret_cast<const f32x4*>(X + brow * kXS + 16 * h);
+#if HN_SPLIT_W
+  // split-f32 (hn_common.h): K = 16 chunk c, element j of lane half h = point 16h + 8c + j
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const SP<HN_SPLIT_W> a = splitn<HN_SPLIT_W>(pa[2 * c], pa[2 * c + 1]);
+    const SP<HN_SPLIT_W> b = splitn<HN_SPLIT_W>(pb[2 * c], pb[2 * c + 1]);
+    acc = mfma_split<HN_SPLIT_W>(a, b, acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return acc;
+#endif
   f32x4 an = pa[0], bn = pb[0];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -381,33 +392,41 @@ HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
 }
 
 // ---- weight-fragment stream ----------------------------------------------
-// A tile's 15 data-path GEMMs read 74 packed A-fragment groups (4 k-steps =
-// one 1-KiB dwordx4 load per wave) in a fixed order, padded to 76 so that a
-// 4-deep ring lines up with the tile period.  The ring keeps the next 4
+// A tile's 15 data-path GEMMs read their packed A-fragment groups (one 1-KiB
+// dwordx4 load per wave: 4 f32 k-steps, or one bf16 part of 8 k-steps) in a
+// fixed order (92 groups at HN_SPLIT_F = 3, HN_SPLIT_B = 2), padded to a
+// multiple of the ring depth so that the ring lines up with the tile period.  The ring keeps the next 4
 // groups (16 MFMAs, ~1000 cycles) in flight across GEMM, tile and unit
 // boundaries: no GEMM starts on an exposed L2 latency at one wave per SIMD.
 struct GemmSeg {
-  int off, ks, ob;
+  int r, ob;   // region (hn_mlp.h), output block
 };
-constexpr GemmSeg kSegs[] = {{G_F0, 16, 0}, {G_F0, 16, 1}, {G_F1, 32, 0}, {G_F2G, 8, 0}, {G_F2G, 8, 1},
-                             {G_F3, 32, 0}, {G_F3, 32, 1}, {G_B4, 4, 0},  {G_B4, 4, 1},  {G_B3, 32, 0},
-                             {G_B3, 32, 1}, {G_B2G, 32, 0}, {G_B1, 8, 0}, {G_B1, 8, 1},  {G_B0, 32, 0}};
+constexpr GemmSeg kSegs[] = {{R_F0, 0}, {R_F0, 1}, {R_F1, 0}, {R_F2G, 0}, {R_F2G, 1}, {R_F3, 0}, {R_F3, 1},
+                             {R_B4, 0}, {R_B4, 1}, {R_B3, 0}, {R_B3, 1}, {R_B2G, 0}, {R_B1, 0}, {R_B1, 1},
+                             {R_B0, 0}};
+constexpr int kNSegs = sizeof(kSegs) / sizeof(kSegs[0]);
+constexpr int seg_start(int i) {   // first group of segment i in the stream
+  int n = 0;
+  for (int j = 0; j < i; ++j) n += reg_gpo(kSegs[j].r);
+  return n;
+}
 #ifndef HN_WRING
 #define HN_WRING 4
 #endif
-constexpr int kTileGroups = 74, kRing = HN_WRING;
+constexpr int kTileGroups = seg_start(kNSegs), kRing = HN_WRING;
 constexpr int kTilePeriod = (kTileGroups + kRing - 1) / kRing * kRing;   // pad groups keep slots static
 constexpr int group_off(int idx) {
   idx %= kTilePeriod;
   if (idx >= kTileGroups) idx = 0;              // pad groups re-read group 0
   for (const GemmSeg& g : kSegs) {
-    const int n = g.ks / 4;
-    if (idx < n) return g.off + (g.ob * n + idx) * 256;
+    const int n = reg_gpo(g.r);
+    if (idx < n) return reg_off(g.r) + (g.ob * n + idx) * 256;
     idx -= n;
   }
   return 0;
 }
-static_assert(group_off(kTileGroups - 1) == G_B0 + 7 * 256, "GEMM sequence");
+static_assert(group_off(kTileGroups - 1) == G_B0 + (reg_gpo(R_B0) - 1) * 256, "GEMM sequence");
+static_assert(HN_SPLIT_F != 3 || HN_SPLIT_B != 2 || (kTileGroups == 92 && G_END == 30208), "layout");
 
 struct WRing {
   f32x4 b[kRing];
@@ -416,17 +435,6 @@ struct WRing {
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
   return *reinterpret_cast<const f32x4*>(opaque_ptr(P) + off + 4 * lane);
 }
-HN_DEV void wring_prime(WRing& w, const float* P, int lane) {
-#pragma unroll
-  for (int j = 0; j < kRing; ++j) w.b[j] = wload(P, group_off(j), lane);
-}
-template <int IDX>
-HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
-  const f32x4 a = w.b[IDX % kRing];
-  w.b[IDX % kRing] = wload(P, group_off(IDX + kRing), lane);
-  return a;
-}
-
 template <int I, int N, typename F>
 HN_DEV void static_for(F&& f) {
   if constexpr (N > 0) {
@@ -435,16 +443,47 @@ HN_DEV void static_for(F&& f) {
   }
 }
 
-// acc += A(groups START .. START + KS/4 of the stream) . B, bval(s) = B operand of k-step s
-template <int KS, int START, typename BF>
-HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
-  static_for<0, KS / 4>([&](auto gc) {
-    constexpr int g = decltype(gc)::value;
-    const f32x4 a = wring_take<START + g>(w, P, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
-    __builtin_amdgcn_sched_barrier(0);
+// (offsets are constexpr-evaluated: left to the optimiser, the region
+// arithmetic of group_off stays as scalar loops in the kernel)
+HN_DEV void wring_prime(WRing& w, const float* P, int lane) {
+  static_for<0, kRing>([&](auto jc) {
+    constexpr int j = decltype(jc)::value, off = group_off(j);
+    w.b[j] = wload(P, off, lane);
   });
+}
+template <int IDX>
+HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
+  constexpr int off = group_off(IDX + kRing);
+  const f32x4 a = w.b[IDX % kRing];
+  w.b[IDX % kRing] = wload(P, off, lane);
+  return a;
+}
+
+// acc += A(segment SEG of the stream) . B, bval(s) = B operand of f32 k-step s
+template <int SEG, typename BF>
+HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
+  constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = reg_ns(R), START = seg_start(SEG);
+  if constexpr (NS > 0) {                       // split-f32: NS groups per K = 16 chunk
+    static_for<0, KS / 8>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      SP<NS> a;
+      static_for<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        a.p[q] = as_bf16x8(wring_take<START + NS * c + q>(w, P, lane));
+      });
+      const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
+      acc = mfma_split<NS>(a, b, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  } else {
+    static_for<0, KS / 4>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      const f32x4 a = wring_take<START + g>(w, P, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
   return acc;
 }
 
@@ -470,30 +509,30 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   // ---- forward recompute (models.py:151-174) ----
   put_rows(X, kRF, feat, lane);
   f32x16 h0[2];
-  h0[0] = gemm_w<16, 0>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
+  h0[0] = gemm_w<0>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
   relu_bits(h0[0], mh0, 0);
   put_rows(X, kRH0, h0[0], lane);
-  h0[1] = gemm_w<16, 4>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
+  h0[1] = gemm_w<1>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
   relu_bits(h0[1], mh0, 1);
   put_rows(X, kRH0 + 32, h0[1], lane);
-  const f32x16 s1 = gemm_w<32, 8>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
+  const f32x16 s1 = gemm_w<2>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
 #pragma unroll
   for (int r = 0; r < 8; ++r) {                 // geo rows 1..15 -> image rows 16..30
     const int row = row_of(r, h);
     if (row >= 1) X[(kRC0in + 15 + row) * kXS + p] = s1[r];
   }
   f32x16 c0[2];
-  c0[0] = gemm_w<8, 16>(wr, P, c0sh[0], lane, [&](int s) { return s1[s]; });
+  c0[0] = gemm_w<3>(wr, P, c0sh[0], lane, [&](int s) { return s1[s]; });
   relu_bits(c0[0], mc0, 0);
   put_rows(X, kRC0, c0[0], lane);
-  c0[1] = gemm_w<8, 18>(wr, P, c0sh[1], lane, [&](int s) { return s1[s]; });
+  c0[1] = gemm_w<4>(wr, P, c0sh[1], lane, [&](int s) { return s1[s]; });
   relu_bits(c0[1], mc0, 1);
   put_rows(X, kRC0 + 32, c0[1], lane);
   {
-    f32x16 c1 = gemm_w<32, 20>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    f32x16 c1 = gemm_w<5>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
     relu_bits(c1, mc1, 0);
     put_rows(X, kRC1, c1, lane);
-    c1 = gemm_w<32, 28>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    c1 = gemm_w<6>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
     relu_bits(c1, mc1, 1);
     put_rows(X, kRC1 + 32, c1, lane);
   }
@@ -509,8 +548,8 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   dw.c2[1] = wgrad(X, rc2, kRC1 + 32 + i, dw.c2[1], lane);
   const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
   f32x16 dc1[2];
-  dc1[0] = gemm_w<4, 36>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
-  dc1[1] = gemm_w<4, 37>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+  dc1[0] = gemm_w<7>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+  dc1[1] = gemm_w<8>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
   mask_bits(dc1[0], mc1, 0);
   mask_bits(dc1[1], mc1, 1);
   lds_fence_wave();
@@ -524,9 +563,9 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     for (int kb = 0; kb < 2; ++kb)
       dw.c1[2 * nb + kb] = wgrad(X, kRC1 + 32 * nb + i, kRC0 + 32 * kb + i, dw.c1[2 * nb + kb], lane);
   f32x16 dc0[2];
-  dc0[0] = gemm_w<32, 38>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+  dc0[0] = gemm_w<9>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
   mask_bits(dc0[0], mc0, 0);
-  dc0[1] = gemm_w<32, 46>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+  dc0[1] = gemm_w<10>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
   mask_bits(dc0[1], mc0, 1);
   lds_fence_wave();
   // ---- color_net.0: X = [sh16 | geo15] (dc0 image over the c0 rows) ----
@@ -535,7 +574,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   lds_fence_wave();
   dw.c0[0] = wgrad(X, kRC0 + i, kRC0in + i, dw.c0[0], lane);
   dw.c0[1] = wgrad(X, kRC0 + 32 + i, kRC0in + i, dw.c0[1], lane);
-  f32x16 ds1 = gemm_w<32, 54>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+  f32x16 ds1 = gemm_w<11>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
   // ---- sigma_net.1 (ds1 image over the c1 rows; rows 16..31 are zero) ----
   put_rows(X, kRC1, ds1, lane);
@@ -543,8 +582,8 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   dw.s1[0] = wgrad(X, kRC1 + i, kRH0 + i, dw.s1[0], lane);
   dw.s1[1] = wgrad(X, kRC1 + i, kRH0 + 32 + i, dw.s1[1], lane);
   f32x16 dh0[2];
-  dh0[0] = gemm_w<8, 62>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
-  dh0[1] = gemm_w<8, 64>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
+  dh0[0] = gemm_w<12>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
+  dh0[1] = gemm_w<13>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
   mask_bits(dh0[0], mh0, 0);
   mask_bits(dh0[1], mh0, 1);
   // ---- sigma_net.0 (dh0 image over the c0 rows) ----
@@ -553,7 +592,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   lds_fence_wave();
   dw.s0[0] = wgrad(X, kRC0 + i, kRF + i, dw.s0[0], lane);
   dw.s0[1] = wgrad(X, kRC0 + 32 + i, kRF + i, dw.s0[1], lane);
-  const f32x16 dfeat = gemm_w<32, 66>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  const f32x16 dfeat = gemm_w<14>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
   static_for<kTileGroups, kTilePeriod - kTileGroups>([&](auto gc) {   // pad groups: keep the ring
     (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
   });
@@ -1014,7 +1053,7 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   f32x16 c0sh[2];
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob)
-    c0sh[ob] = gemm<8>(P, G_F2S, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+    c0sh[ob] = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
   const int ctile = (fine ? kSc / 32 : 0) + tile0;
   float zq[2] = {0.f, 0.f};
   int srcq[2] = {0, 0};
@@ -1028,8 +1067,8 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   f32x16 feat, featn;
   load_feat(k.feat, ray, ctile, lane, feat);
   load_feat(k.feat, ray, ctile + 1, lane, featn);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  static_for<0, 2>([&](auto tc) {   // unrolled: the ring's slots and the per-tile arrays stay static
+    constexpr int t = decltype(tc)::value;
     if (t == 0) HN_LAP(pc, unit);
     const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
     HN_LAP(pc, mlp);
@@ -1055,7 +1094,7 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
         dst[16 + l] = dfeat[2 * m + 1];
       }
     }
-  }
+  });
 }
 
 // Composite backward pre-pass (raw2outputs backward, run_nerf_helpers.py:577-628

@@ -64,7 +64,7 @@ typedef struct hn_mlp_grad {
 } hn_mlp_grad;
 
 #define HN_MLP_PARAMS 9344          /* 2048 + 1024 + 1984 + 4096 + 192 */
-#define HN_MLP_PACKED_FLOATS 24064  /* MFMA fragment-ordered copy, per net */
+#define HN_MLP_PACKED_FLOATS 30208  /* MFMA fragment-ordered copy (split-f32 bf16 parts), per net */
 
 int32_t hn_abi_version(void);
 const char* hn_status_string(int32_t status);
