@@ -69,13 +69,27 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 // acc += A(region R, block ob) . B where bval(s) is the B operand of f32 k-step s.
 // The next A fragments are loaded while the current ones' MFMAs run; the
 // scheduling barrier stops hipcc from hoisting all loads (register blowup).
+#ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk
+#define HN_GEMM_PF 1
+#endif
 template <int R, typename BF>
 HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF bval) {
   constexpr int KS = kRegKS[R], NS = reg_ns(R), GPO = reg_gpo(R), OFF = reg_off(R);
   // opaque BEFORE the offset: keeps hipcc from precomputing ~50 uniform GEMM
   // base addresses at the top of the tile loop (SGPR pairs that then spill)
   const float* base = opaque_ptr(P) + OFF + ob * GPO * 256 + lane * 4;
-  if constexpr (NS > 0) {                       // split-f32 on the bf16 MFMA
+  if constexpr (NS > 0 && !HN_GEMM_PF) {        // split-f32, fragments loaded at use
+#pragma unroll
+    for (int c = 0; c < KS / 8; ++c) {
+      SP<NS> a;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + (NS * c + q) * 256));
+      const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
+      acc = mfma_split<NS>(a, b, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+  } else if constexpr (NS > 0) {                // split-f32 on the bf16 MFMA
     SP<NS> an;
 #pragma unroll
     for (int q = 0; q < NS; ++q) an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + q * 256));

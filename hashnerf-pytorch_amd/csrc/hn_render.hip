@@ -342,8 +342,14 @@ constexpr int kB1Img = kMW * kRRows * kXS;                 // floats (112,320 B)
 constexpr int kSlots = HN_SLOTS;
 constexpr int kSlotZ = 32 * kXS, kSlotR = kSlotZ + 32, kSlotF = kSlotR + 8;
 constexpr int kVoxF = 16 * 16 * 8;                         // scatter wave's voxel buffer
+// Compacted atomic issue (HN_COMPACT, scatter_level_x): a ring of kQ {byte
+// offset, value} slots right after the voxel buffer.
+#ifndef HN_COMPACT
+#define HN_COMPACT 0
+#endif
+constexpr int kQ = HN_COMPACT ? 512 : 0;
 constexpr int kSyncInts = 5 + 2 * kSlots;
-constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + kGsLds + kSyncInts;
+constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + 2 * kQ + kGsLds + kSyncInts;
 static_assert(kB1LdsF * 4 <= 160 * 1024, "LDS budget");
 static_assert(kB1Img >= W_END, "final dW reduction reuses the images");
 static_assert(kRRows * kXS % 4 == 0 && kXS % 4 == 0 && kSlotF % 4 == 0, "b128 alignment");
@@ -663,9 +669,59 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 // point's voxel {cell x, cell y * PY, cell z * PZ, w x, y, z} from the compact
 // pass (the prime products are precomputed there: (c + 1) * P = c * P + P,
 // and c -> c * P is a bijection, so run heads compare the products).
+// Compacted issue queue of the scatter wave: head / tail are wave-uniform
+// running counts of slots read / written.  Full 64-slot batches are read
+// into registers after a level's queue writes and issued as atomics at the
+// start of the next level, so the LDS read latency hides under that level's
+// VALU work instead of stalling the wave.
+struct AQ {
+  float2* buf;
+  uint32_t head, tail;
+  uint32_t nb;      // batches held in e[]
+  float2 e[4];
+};
+#ifndef HN_QCAP   // compacted atomic wave-instructions in flight before the next is issued
+#define HN_QCAP 4
+#endif
+HN_DEV void aq_atomic(float* __restrict__ dtable, float2 e, bool on) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HN_QCAP) : "memory");
+  if (on) atomic_add_f32(reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) + __float_as_uint(e.x)), e.y);
+}
+// issue the batches read earlier
+HN_DEV void aq_flush_regs(float* __restrict__ dtable, AQ& q) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if ((uint32_t)b < q.nb) aq_atomic(dtable, q.e[b], true);
+  q.nb = 0;
+}
+// read every full batch now in the queue (at most 4: a level adds <= 256 slots)
+HN_DEV void aq_read(AQ& q, int lane) {
+  asm volatile("" ::: "memory");                 // after the queue writes (LDS is in order per wave)
+  const uint32_t n = (q.tail - q.head) >> 6;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if ((uint32_t)b < n) q.e[b] = q.buf[(q.head + 64u * (uint32_t)b + (uint32_t)lane) & (uint32_t)(kQ - 1)];
+  q.head += 64u * n;
+  q.nb = n;
+}
+// end of the stream: everything still held or queued
+HN_DEV void aq_drain(float* __restrict__ dtable, AQ& q, int lane) {
+  aq_flush_regs(dtable, q);
+  aq_read(q, lane);
+  aq_flush_regs(dtable, q);
+  const uint32_t n = q.tail - q.head;
+  if (n) {
+    asm volatile("" ::: "memory");
+    const float2 e = q.buf[(q.head + (uint32_t)lane) & (uint32_t)(kQ - 1)];
+    aq_atomic(dtable, e, (uint32_t)lane < n);
+    q.head += n;
+  }
+}
+
 HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const f32x4 v0, const float2 v1,
-                            uint32_t l, float gl, int lane) {
-  const int pp = lane & 15, f = (lane >> 4) & 1, xi = lane >> 5;
+                            uint32_t l, float gl, int lane, AQ& aq) {
+  const int pp = lane & 15, xi = lane >> 5;
+  [[maybe_unused]] const int f = (lane >> 4) & 1;
   const uint32_t cx = (uint32_t)__float_as_int(v0.x), y0 = (uint32_t)__float_as_int(v0.y),
                  z0 = (uint32_t)__float_as_int(v0.z);
   const float w[3] = {v0.w, v1.x, v1.y};
@@ -750,6 +806,33 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
 #endif
 #if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
   if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
+#elif HN_COMPACT
+  // Compacted issue: the run heads' adds are queued densely in LDS and go out
+  // as full 64-lane atomic wave-instructions across levels, tiles and rays
+  // (coarse levels have 1-3 heads per 16 points: one instruction per corner
+  // row per level carried only 4-12 active lanes).  Queue order: corner row
+  // c, head rank r, lane-in-unit s = 2 xi + f -> slot 4 nh c + 4 r + s, so a
+  // head's x-pair and both features stay adjacent (one 64-B segment) and the
+  // queue writes of one row are consecutive (conflict-free).
+  static_assert(!HN_NMERGE, "the neighbour merge is not wired into the compacted queue");
+  (void)gfin;
+  {
+    aq_flush_regs(dtable, aq);                   // the batches read at the previous level
+    const uint32_t row0 = l << g.log2T;
+    const uint32_t nh = (uint32_t)__builtin_popcount(pm);
+    if (head) {
+      const uint32_t rk = (uint32_t)__builtin_popcount(pm & ((1u << pp) - 1u));
+      const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
+                              (hx ^ y1 ^ z1) & mask};
+      const uint32_t base = aq.tail + 4u * rk + (uint32_t)(lane >> 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        aq.buf[(base + 4u * nh * (uint32_t)c) & (uint32_t)(kQ - 1)] =
+            make_float2(__uint_as_float((row0 + hh[c]) * 8u + 4u * (uint32_t)f), cv[c]);
+    }
+    aq.tail += 16u * nh;
+    aq_read(aq, lane);
+  }
 #else
   if (head) {
     const uint32_t row0 = l << g.log2T;
@@ -893,7 +976,7 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 
 // The table-gradient scatter of one slot (embedding_dense_backward of
 // hash_encoding.py:106 + trilinear backward); V = 2048-float voxel buffer.
-HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl) {
+HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl, AQ& aq) {
   const int lane = lane_id();
   const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
   Ray r;
@@ -943,7 +1026,7 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
         v0 = *reinterpret_cast<const f32x4*>(vs + (l + 1) * 128);
         v1 = *reinterpret_cast<const float2*>(vs + (l + 1) * 128 + 4);
       }
-      scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane);
+      scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
       if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -975,7 +1058,9 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
     if (lds_load(&q.freed[tn % kSlots]) < tn / kSlots) {   // next slot still occupied
       if (lane == 0) atomicAdd(q.selfc, 1);
       fill_slot(X, r, z, dfeat, tw);
-      scatter_slot(k, X, X + kSlotF, q.gsl);
+      static_assert(!HN_MW_SELF || !HN_COMPACT, "the compacted queue belongs to the scatter wave");
+      AQ none{nullptr, 0u, 0u, 0u, {}};
+      scatter_slot(k, X, X + kSlotF, q.gsl, none);
       return;
     }
   }
@@ -994,6 +1079,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
 // only grow and a tile is counted before it is handled, so tick + selfc ==
 // n_tiles with t >= tick means no ticket t will ever come.
 HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
+  AQ aq{reinterpret_cast<float2*>(V + kVoxF), 0u, 0u, 0u, {}};
   for (int t = 0;; ++t) {
     const int s = t % kSlots;
 #if HN_PROFILE
@@ -1015,9 +1101,10 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
 #endif
     if (!have) break;
     const float* S = q.slots + s * kSlotF;
-    scatter_slot(k, S, V, q.gsl);
+    scatter_slot(k, S, V, q.gsl, aq);
     ring_publish(&q.freed[s], t / kSlots + 1);
   }
+  if (HN_COMPACT) aq_drain(k.d_table, aq, lane_id());
 }
 
 HN_DEV void wait_flag(int* flag, int need) {
@@ -1210,7 +1297,7 @@ void render_bwd_kernel(B1K k) {
   float* X = smem + wave * kRRows * kXS;
   float* slots = smem + kB1Img;
   float* V = slots + kSlots * kSlotF;
-  float* gsl = V + kVoxF;
+  float* gsl = V + kVoxF + 2 * kQ;               // [voxel buffer | atomic queue | grid sizes | sync]
   // [0] coarse rays done, [1] fine units taken, [2] ring tickets, [3] dW buffer zeroed,
   // [4] self-scattered tiles, [5..) ready, freed
   int* sync = reinterpret_cast<int*>(gsl + kGsLds);
