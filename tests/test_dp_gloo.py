@@ -63,15 +63,15 @@ def _grads(O, box, tab, wc, wf, rb, t_rand, u, target, mv, T, loss_fn):
     return tab, [wc[k] for k in O.MLP_KEYS] + [wf[k] for k in O.MLP_KEYS]
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, T=12):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import sys
     sys.path.insert(0, ROOT)
     import hn_loader
     hn_loader.load()
-    from hashnerf_pytorch_amd.train import allreduce_grads, dp_loss
-    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene()
+    from hashnerf_pytorch_amd.train import allreduce_grads, dp_loss, live_rows
+    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene(T=T)
     B = rb.shape[0]
     sl = slice(rank * B // world, (rank + 1) * B // world)
 
@@ -82,7 +82,8 @@ def _worker(rank, world, port, out_path):
         return dp_loss(mse, mse0, ent, world, 1e-3, tv if rank == 0 else None, 1e-2)
 
     tab_g, mlp = _grads(O, box, tab, wc, wf, rb[sl], t_rand[sl], u[sl], target[sl], mv, T, loss_fn)
-    allreduce_grads(tab_g, mlp)
+    # T=16: levels 0-3 go through the compacted live-row bucket
+    allreduce_grads(tab_g, mlp, live=live_rows(O.level_resolutions(16, 16, 512), T))
     if rank == 0:
         torch.save({"table": tab_g.grad, "mlp": [p.grad for p in mlp]}, out_path)
     dist.barrier()
@@ -118,11 +119,12 @@ def _allreduce_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_dp_gradient_equals_global_batch(tmp_path):
+@pytest.mark.parametrize("T", [12, 16])
+def test_dp_gradient_equals_global_batch(tmp_path, T):
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path / "dp.pt")), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, port, str(tmp_path / "dp.pt"), T), nprocs=2, join=True)
     got = torch.load(tmp_path / "dp.pt", weights_only=True)
-    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene()
+    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene(T=T)
 
     def ref_loss(ret, tgt, tv):   # run_nerf.py:612-636 on the whole batch
         return (torch.mean((ret["rgb_map"] - tgt) ** 2) + torch.mean((ret["rgb0"] - tgt) ** 2)
@@ -135,3 +137,29 @@ def test_dp_gradient_equals_global_batch(tmp_path):
     for a, p in zip(got["mlp"], mlp):
         e = (a - p.grad).norm() / p.grad.norm()
         assert e < 1e-5, e
+
+
+def test_live_rows_cover_every_gradient():
+    """The rows allreduce_grads leaves out (train.live_rows) carry no gradient:
+    render + TV backward of the oracle with samples outside the bbox (clamped
+    corners, hash_encoding.py:66-76) and TV cubes at the far corner of the grid."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import live_rows
+    O, box, tab, wc, wf, rb, t_rand, u, target, mv, T = _scene(T=16)
+    res = O.level_resolutions(16, 16, 512)
+    mv = torch.stack([torch.tensor([int(r) - int(O.tv_cube(l, 16, 16, 512)[1]) - 1] * 3) for l, r in enumerate(res)])
+
+    def loss_fn(ret, tgt, tv):
+        return (torch.mean((ret["rgb_map"] - tgt) ** 2) + 1e-3 * ret["sparsity_loss"].sum() + 1e-2 * tv)
+
+    tab_g, _ = _grads(O, box, tab, wc, wf, rb, t_rand, u, target, mv, T, loss_fn)
+    n_lv, rows = live_rows(res, T)
+    assert n_lv == 4
+    head = tab_g.grad[:n_lv].reshape(-1, 2)
+    dead = torch.ones(head.shape[0], dtype=torch.bool)
+    dead[rows] = False
+    assert head[~dead].abs().sum() > 0
+    assert torch.count_nonzero(head[dead]) == 0
