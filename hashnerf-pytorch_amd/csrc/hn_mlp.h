@@ -72,6 +72,9 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 #ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk
 #define HN_GEMM_PF 1
 #endif
+#ifndef HN_GEMM_SWP  // 1: the next chunk's B split is interleaved with this chunk's MFMAs
+#define HN_GEMM_SWP 0
+#endif
 template <int R, typename BF>
 HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF bval) {
   constexpr int KS = kRegKS[R], NS = reg_ns(R), GPO = reg_gpo(R), OFF = reg_off(R);
@@ -93,6 +96,9 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
     SP<NS> an;
 #pragma unroll
     for (int q = 0; q < NS; ++q) an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + q * 256));
+#if HN_GEMM_SWP
+    SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
+#endif
 #pragma unroll
     for (int c = 0; c < KS / 8; ++c) {
       const SP<NS> a = an;
@@ -101,8 +107,23 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
         for (int q = 0; q < NS; ++q)
           an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + (NS * (c + 1) + q) * 256));
       }
+#if HN_GEMM_SWP
+      // the next chunk's split (VALU) goes into this chunk's MFMA gaps
+      SP<NS> bn = b;
+      if (c + 1 < KS / 8) bn = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
+      acc = mfma_split<NS>(a, b, acc);
+      if (c + 1 < KS / 8) {
+#pragma unroll
+        for (int i = 0; i < (NS == 3 ? 6 : 3); ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, NS == 3 ? 6 : 5, 0);   // then VALU
+        }
+      }
+      b = bn;
+#else
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
       acc = mfma_split<NS>(a, b, acc);
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
