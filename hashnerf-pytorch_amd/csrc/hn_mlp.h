@@ -1,14 +1,16 @@
-// hn_mlp.h -- NeRFSmall (models.py:96-174) on gfx950 f32 MFMA, one wave per
+// hn_mlp.h -- NeRFSmall (models.py:96-174) on the gfx950 MFMA, one wave per
 // 32-point tile.
 //
 // Orientation: every layer computes Y[out][pt] = W[out][in] . X[in][pt] with
-// v_mfma_f32_32x32x2_f32, so points sit on the MFMA columns (lane & 31) and
-// neurons on the accumulator rows.  A layer's D tile is then directly the B
-// operand of the next layer (and of the W^T data-gradient products): lane
-// half h at k-step s supplies its own register s, i.e. input row
-// row_of(s & 15, h) of tile s >> 4 -- no lane movement between layers.  The
-// weights are pre-packed ("fragment order") so the A operands of four k-steps
-// are one coalesced 1-KiB dwordx4 load: packed[gemm][ob][s/4][lane][s%4].
+// 32x32 MFMA tiles (v_mfma_f32_32x32x16_bf16 on split-f32 operands, see
+// hn_common.h; v_mfma_f32_32x32x2_f32 in the f32 build), so points sit on the
+// MFMA columns (lane & 31) and neurons on the accumulator rows.  A layer's D
+// tile is then directly the B operand of the next layer (and of the W^T
+// data-gradient products): lane half h at f32 k-step s supplies its own
+// register s, i.e. input row row_of(s & 15, h) of tile s >> 4 -- no lane
+// movement between layers.  The weights are pre-packed ("fragment order") so
+// the A operands of a group are one coalesced 1-KiB dwordx4 load (regions and
+// groups below).
 //
 // Layouts per lane (p = lane & 31 = point, h = lane >> 5):
 //   feat  f32x16: reg r = feature row_of(r,h) = (level tile_level(r>>1,h), r&1)
