@@ -49,7 +49,12 @@ enum : int { R_F0, R_F1, R_F2G, R_F2S, R_F3, R_F4, R_B4, R_B3, R_B2G, R_B2S, R_B
 //  B4 color_net.2^T  B3 color_net.1^T  B2G/B2S color_net.0^T geo/sh  B1 sigma_net.1^T  B0 sigma_net.0^T
 constexpr int kRegKS[R_N] = {16, 32, 8, 8, 32, 32, 4, 32, 32, 32, 8, 32};
 constexpr int kRegOB[R_N] = {2, 1, 2, 2, 2, 1, 2, 2, 1, 1, 2, 1};
-constexpr int reg_ns(int r) { return kRegKS[r] % 8 ? 0 : (r < R_B4 ? HN_SPLIT_F : HN_SPLIT_B); }
+#ifndef HN_SPLIT_FC   // parts in the forward colour-net GEMMs (color_net.0-2)
+#define HN_SPLIT_FC HN_SPLIT_F
+#endif
+constexpr int reg_ns(int r) {
+  return kRegKS[r] % 8 ? 0 : (r < R_F2G ? HN_SPLIT_F : (r < R_B4 ? HN_SPLIT_FC : HN_SPLIT_B));
+}
 constexpr int reg_gpo(int r) { return reg_ns(r) ? reg_ns(r) * kRegKS[r] / 8 : kRegKS[r] / 4; }   // groups per OB
 constexpr int reg_off(int r) {
   int o = 0;

@@ -432,7 +432,7 @@ constexpr int group_off(int idx) {
   return 0;
 }
 static_assert(group_off(kTileGroups - 1) == G_B0 + (reg_gpo(R_B0) - 1) * 256, "GEMM sequence");
-static_assert(HN_SPLIT_F != 3 || HN_SPLIT_B != 2 || (kTileGroups == 92 && G_END == 30208), "layout");
+static_assert(HN_SPLIT_F != 3 || HN_SPLIT_FC != 3 || HN_SPLIT_B != 2 || (kTileGroups == 92 && G_END == 30208), "layout");
 
 struct WRing {
   f32x4 b[kRing];
