@@ -139,6 +139,8 @@ def main():
     ap.add_argument("--pretrain", type=int, default=1000,
                     help="untimed training steps before warmup")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--ray-order", type=int, default=1, choices=(0, 1),
+                    help="batch order from the sampler: 1 Morton order of the pixels, 0 draw order")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -176,7 +178,7 @@ def main():
     t_data = time.perf_counter() - t_data
     if "bbox" in cfg:
         data.bounding_box = tuple(torch.tensor(v) for v in cfg["bbox"])
-    tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0)
+    tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0, ray_order=args.ray_order)
 
     for i in range(args.pretrain + args.warmup):
         tr.step(i)

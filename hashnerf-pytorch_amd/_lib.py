@@ -109,6 +109,9 @@ SIGNATURES = {
     "hn_tv_bwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P, _P]),
     "hn_radam_step": (C.c_int32, [C.POINTER(HnRadamTensor), C.c_int32, _P]),
     "hn_sample_rays": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P]),
+    "hn_sample_rays_morton_workspace_bytes": (C.c_size_t, [C.POINTER(HnRaySampler)]),
+    "hn_sample_rays_morton": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P, C.c_size_t,
+                                          _P]),
     "hn_loss_fwd": (C.c_int32, [_P, _P, _P, _P, _P, C.c_int64, _P, C.c_int32, C.c_float, C.c_float,
                                 C.c_float, _P, _P]),
     "hn_loss_bwd": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_float, _P,

@@ -352,6 +352,47 @@ HN_DEV T* opaque_ptr(T* p) {
   return (T*)((__attribute__((address_space(1))) T*)v);
 }
 
+// ---------------------------------------------------------------------------
+// Keyed 4-round Feistel permutation of [0, 2^(2 half)) (pixel sampling without
+// replacement, hn_train.hip; ray scrambling in the render backward) and its
+// inverse.
+// ---------------------------------------------------------------------------
+HN_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+HN_DEV uint32_t feistel(uint32_t x, int half, uint64_t seed) {
+  const uint32_t mask = (1u << half) - 1u;
+  uint32_t L = x >> half, R = x & mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t key = (uint32_t)(seed >> (16 * r)) ^ (0x9e3779b9u * (uint32_t)(r + 1));
+    const uint32_t F = mix32(R ^ key) & mask;
+    const uint32_t t = R;
+    R = L ^ F;
+    L = t;
+  }
+  return (L << half) | R;
+}
+
+HN_DEV uint32_t feistel_inv(uint32_t x, int half, uint64_t seed) {
+  const uint32_t mask = (1u << half) - 1u;
+  uint32_t L = x >> half, R = x & mask;
+#pragma unroll
+  for (int r = 3; r >= 0; --r) {
+    const uint32_t key = (uint32_t)(seed >> (16 * r)) ^ (0x9e3779b9u * (uint32_t)(r + 1));
+    const uint32_t t = L;
+    L = R ^ (mix32(t ^ key) & mask);
+    R = t;
+  }
+  return (L << half) | R;
+}
+
 inline int32_t hip_status(hipError_t e) { return e == hipSuccess ? HN_OK : HN_E_HIP + (int32_t)e; }
 
 HN_DEV f32x16 zero16() {

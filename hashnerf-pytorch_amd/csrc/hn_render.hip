@@ -51,6 +51,7 @@ struct RenderK {
 // Arguments of the backward MLP kernel (kept lean: every field lives in SGPRs).
 struct B1K {
   int64_t B;
+  int32_t scramble;     // Feistel half-width of the chunk-position -> ray permutation, 0: identity
   int white;
   const float* rays;
   const float *noise_c, *noise_f;
@@ -161,6 +162,15 @@ constexpr int kFZc = 0, kFZsrc = 64, kFZs = 256, kFRaw = 448, kFW = 1216, kFBins
 #ifndef HN_FWD_WAVES_PER_SIMD
 #define HN_FWD_WAVES_PER_SIMD 4
 #endif
+#ifndef HN_BWD_CHUNK   // 1: each backward block owns a contiguous chunk of the batch
+#define HN_BWD_CHUNK 1
+#endif
+#ifndef HN_BWD_SCRAMBLE   // 1: ... of a pseudo-randomly permuted order of the batch
+#define HN_BWD_SCRAMBLE 1
+#endif
+#ifndef HN_XCD_MAP   // 1: consecutive ray groups of the batch on one XCD (shared L2)
+#define HN_XCD_MAP 1
+#endif
 // 4 waves per SIMD (<= 128 registers; the few spills sit outside the tile
 // loops): one ray per wave, so a 4096-ray batch is exactly one round on 256
 // CUs (3 waves: 0.427 ms, a 1/3-occupied second round; 4: 0.418 ms)
@@ -183,7 +193,15 @@ void render_fwd_kernel(RenderK k) {
   float* gsl = smem + kFwdWaves * kFLds;
   stage_grid_sizes(k.g, gsl);
   __syncthreads();
+#if HN_XCD_MAP
+  // XCD-aware: workgroup b runs on XCD b % 8, so consecutive ray groups of a
+  // spatially ordered batch go to one XCD and share its L2
+  const int64_t nb = gridDim.x;
+  const int64_t grp = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+  const int64_t ray = grp * kFwdWaves + wave;
+#else
   const int64_t ray = (int64_t)blockIdx.x * kFwdWaves + wave;
+#endif
   if (ray >= k.B) return;
   float* L = smem + wave * kFLds;
   float* zc = L + kFZc;
@@ -1307,6 +1325,23 @@ void render_bwd_kernel(B1K k) {
   const Ring ring{slots, &sync[2], &sync[4], &sync[5], &sync[5 + kSlots], gsl};
   const int64_t nb = gridDim.x;
   const int n_rays = k.B > (int64_t)blockIdx.x ? (int)((k.B - 1 - blockIdx.x) / nb + 1) : 0;
+  // ray of the block's i-th unit: a contiguous chunk per block when the
+  // batch divides evenly, so the rays in flight at one time across the chip
+  // are far apart in a spatially ordered batch (concurrent atomics on the
+  // same rows serialize at the memory side); strided otherwise
+  const bool chunked = HN_BWD_CHUNK && k.B % nb == 0;
+  auto block_ray = [&](int64_t i) -> int64_t {
+    if (!chunked) return (int64_t)blockIdx.x + i * nb;
+    // a fixed pseudo-random permutation of the batch scatters both the rays in
+    // flight across the chip (one per block) and a block's consecutive rays
+    uint32_t x = (uint32_t)((int64_t)blockIdx.x * (k.B / nb) + i);
+    if (k.scramble) {
+      do {
+        x = feistel(x, k.scramble, 0x5bd1e995u);
+      } while ((int64_t)x >= k.B);
+    }
+    return (int64_t)x;
+  };
   DW dw;
   dw_zero(dw);
   WRing wr;
@@ -1323,7 +1358,7 @@ void render_bwd_kernel(B1K k) {
     if (wave == 0) {
       wring_prime(wr, k.Pc, lane);
       for (int i = 0; i < n_rays; ++i) {
-        b1_unit<kSc>(k, blockIdx.x + i * nb, 0, X, dw, wr, nullptr, pc);
+        b1_unit<kSc>(k, block_ray(i), 0, X, dw, wr, nullptr, pc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this ray's feature grads are in L2
         if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -1336,7 +1371,7 @@ void render_bwd_kernel(B1K k) {
       if (lane == 0) u = atomicAdd(&sync[1], 1);
       u = __builtin_amdgcn_readfirstlane(u);
       if (u >= 3 * n_rays) break;
-      b1_unit<kSf>(k, blockIdx.x + (int64_t)(u / 3) * nb, u % 3, X, dw, wr, &ring, pc, &sync[0], u / 3 + 1);
+      b1_unit<kSf>(k, block_ray(u / 3), u % 3, X, dw, wr, &ring, pc, &sync[0], u / 3 + 1);
     }
     // block reduction of the MLP waves' fine dW into wave 0's image, inside
     // this branch: the accumulators must not be live in the scatter wave's
@@ -1497,6 +1532,12 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   B1K k;
   k.B = a->n_rays;
+  k.scramble = 0;
+  if (HN_BWD_SCRAMBLE && a->n_rays > 1) {
+    int bits = 2;
+    while ((1ll << bits) < a->n_rays) bits += 2;
+    k.scramble = bits / 2;
+  }
   k.white = cfg->white_bkgd;
   k.rays = a->rays; k.noise_c = a->noise_c; k.noise_f = a->noise_f;
   k.Pc = Pc; k.Pf = Pf;

@@ -16,29 +16,6 @@ namespace hn {
 // walking, is a bijection of [0, M); sample i is perm(i), so the n samples
 // are distinct for any seed.
 // ---------------------------------------------------------------------------
-HN_DEV uint32_t mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-HN_DEV uint32_t feistel(uint32_t x, int half, uint64_t seed) {
-  const uint32_t mask = (1u << half) - 1u;
-  uint32_t L = x >> half, R = x & mask;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const uint32_t key = (uint32_t)(seed >> (16 * r)) ^ (0x9e3779b9u * (uint32_t)(r + 1));
-    const uint32_t F = mix32(R ^ key) & mask;
-    const uint32_t t = R;
-    R = L ^ F;
-    L = t;
-  }
-  return (L << half) | R;
-}
-
 __global__ __launch_bounds__(256) void sample_rays_kernel(hn_ray_sampler s, const float* __restrict__ image,
                                                           const float* __restrict__ c2w, int64_t n,
                                                           int half, float* __restrict__ rays,
@@ -72,6 +49,99 @@ __global__ __launch_bounds__(256) void sample_rays_kernel(hn_ray_sampler s, cons
   const float* px3 = image + 3 * ((size_t)py * s.W + px);
 #pragma unroll
   for (int a = 0; a < 3; ++a) target[3 * i + a] = px3[a];
+}
+
+// ---------------------------------------------------------------------------
+// The same draw in Morton order of its pixels (window-relative row, column):
+// pixel x is drawn iff perm^-1(x) < n, so walking the Morton indices of the
+// window and compacting the drawn ones lists the draw's set in that order with
+// no sort.  Two launches: per-block counts, then prefix + block scan + emit.
+// ---------------------------------------------------------------------------
+constexpr int kMortonThreads = 1024;
+HN_DEV uint32_t compact_bits16(uint32_t v) {
+  v &= 0x55555555u;
+  v = (v | (v >> 1)) & 0x33333333u;
+  v = (v | (v >> 2)) & 0x0f0f0f0fu;
+  v = (v | (v >> 4)) & 0x00ff00ffu;
+  v = (v | (v >> 8)) & 0x0000ffffu;
+  return v;
+}
+// Morton index m -> drawn pixel (window-relative linear index) or ~0u
+HN_DEV uint32_t morton_drawn(const hn_ray_sampler& s, int half, int64_t n, uint32_t m) {
+  const uint32_t row = compact_bits16(m >> 1), col = compact_bits16(m);
+  if (row >= (uint32_t)s.crop_h || col >= (uint32_t)s.crop_w) return ~0u;
+  const uint32_t M = (uint32_t)s.crop_h * (uint32_t)s.crop_w;
+  const uint32_t x = row * (uint32_t)s.crop_w + col;
+  uint32_t y = x;
+  do {   // inverse of the cycle-walked permutation
+    y = feistel_inv(y, half, s.seed);
+  } while (y >= M);
+  return (int64_t)y < n ? x : ~0u;
+}
+
+__global__ __launch_bounds__(kMortonThreads) void morton_count_kernel(hn_ray_sampler s, int half, int64_t n,
+                                                                      uint32_t n_idx, int* __restrict__ counts) {
+  const uint32_t m = blockIdx.x * kMortonThreads + threadIdx.x;
+  const bool sel = m < n_idx && morton_drawn(s, half, n, m) != ~0u;
+  const int c = __syncthreads_count(sel);
+  if (threadIdx.x == 0) counts[blockIdx.x] = c;
+}
+
+HN_DEV void emit_ray(const hn_ray_sampler& s, const float* __restrict__ image, const float* __restrict__ c2w,
+                     uint32_t x, int64_t r, float* __restrict__ rays, float* __restrict__ target) {
+  const int py = s.crop_y0 + (int)(x / (uint32_t)s.crop_w);
+  const int px = s.crop_x0 + (int)(x % (uint32_t)s.crop_w);
+  // dirs = [(i - cx) / fx, -(j - cy) / fy, -1]; rays_d = sum(dirs * c2w[:3,:3], -1)
+  const float d0 = ((float)px - s.cx) / s.fx;
+  const float d1 = -(((float)py - s.cy) / s.fy);
+  const float d2 = -1.f;
+  float* out = rays + 11 * r;
+  float d[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    d[a] = d0 * c2w[4 * a] + d1 * c2w[4 * a + 1] + d2 * c2w[4 * a + 2];
+    out[a] = c2w[4 * a + 3];
+    out[3 + a] = d[a];
+  }
+  out[6] = s.near;
+  out[7] = s.far;
+  const float nrm = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) out[8 + a] = d[a] / nrm;
+  const float* px3 = image + 3 * ((size_t)py * s.W + px);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) target[3 * r + a] = px3[a];
+}
+
+__global__ __launch_bounds__(kMortonThreads) void morton_emit_kernel(hn_ray_sampler s, const float* __restrict__ image,
+                                                                     const float* __restrict__ c2w, int half,
+                                                                     int64_t n, uint32_t n_idx,
+                                                                     const int* __restrict__ counts,
+                                                                     float* __restrict__ rays,
+                                                                     float* __restrict__ target) {
+  __shared__ int part[kMortonThreads / 64 + 1];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // rays drawn by the earlier blocks
+  uint32_t pre = 0;
+  for (uint32_t b = tid; b < blockIdx.x; b += kMortonThreads) pre += (uint32_t)counts[b];
+  pre = wave_sum(pre);
+  if (lane == 0) part[wave] = (int)pre;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int w = 0; w < kMortonThreads / 64; ++w) base += part[w];
+  __syncthreads();
+  const uint32_t m = blockIdx.x * kMortonThreads + tid;
+  const uint32_t x = m < n_idx ? morton_drawn(s, half, n, m) : ~0u;
+  const bool sel = x != ~0u;
+  const uint64_t bal = __ballot(sel);
+  if (lane == 0) part[wave] = __popcll(bal);
+  __syncthreads();
+  int off = base;
+  for (int w = 0; w < wave; ++w) off += part[w];
+  if (!sel) return;
+  const int64_t r = off + __popcll(bal & ((1ull << lane) - 1ull));
+  emit_ray(s, image, c2w, x, r, rays, target);
 }
 
 // ---------------------------------------------------------------------------
@@ -186,6 +256,51 @@ extern "C" int32_t hn_sample_rays(const hn_ray_sampler* s, const float* image, c
   const unsigned blocks = (unsigned)((n_rays + 255) / 256);
   hipLaunchKernelGGL(sample_rays_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *s, image, c2w, n_rays,
                      bits / 2, rays, target);
+  return hip_status(hipGetLastError());
+}
+
+// Morton-window geometry: 4^k indices cover the window, 1024 per block.
+static bool morton_geometry(const hn_ray_sampler* s, uint32_t& n_idx, unsigned& blocks) {
+  if (s->crop_h <= 0 || s->crop_w <= 0 || s->crop_h > HN_SAMPLER_MORTON_MAX || s->crop_w > HN_SAMPLER_MORTON_MAX)
+    return false;
+  int k = 0;
+  while ((1 << k) < s->crop_h || (1 << k) < s->crop_w) ++k;
+  n_idx = 1u << (2 * k);
+  blocks = (unsigned)((n_idx + kMortonThreads - 1) / kMortonThreads);
+  return true;
+}
+
+extern "C" size_t hn_sample_rays_morton_workspace_bytes(const hn_ray_sampler* s) {
+  uint32_t n_idx;
+  unsigned blocks;
+  if (!s || !morton_geometry(s, n_idx, blocks)) return 0;
+  return (size_t)blocks * sizeof(int);
+}
+
+extern "C" int32_t hn_sample_rays_morton(const hn_ray_sampler* s, const float* image, const float* c2w,
+                                         int64_t n_rays, float* rays, float* target, void* workspace,
+                                         size_t ws_bytes, void* stream) {
+  if (!s) return HN_E_NULL;
+  if (n_rays < 0) return HN_E_SHAPE;
+  if (n_rays == 0) return HN_OK;
+  if (!image || !c2w || !rays || !target) return HN_E_NULL;
+  if (s->H <= 0 || s->W <= 0 || s->crop_h <= 0 || s->crop_w <= 0 || s->crop_y0 < 0 || s->crop_x0 < 0 ||
+      s->crop_y0 + s->crop_h > s->H || s->crop_x0 + s->crop_w > s->W)
+    return HN_E_SHAPE;
+  uint32_t n_idx;
+  unsigned blocks;
+  if (!morton_geometry(s, n_idx, blocks)) return HN_E_SHAPE;
+  const uint64_t M = (uint64_t)s->crop_h * (uint64_t)s->crop_w;
+  if ((uint64_t)n_rays > M) return HN_E_SHAPE;   // without replacement
+  if (!workspace) return HN_E_NULL;
+  if (ws_bytes < (size_t)blocks * sizeof(int)) return HN_E_WORKSPACE;
+  int bits = 2;
+  while ((1ull << bits) < M) bits += 2;
+  int* counts = static_cast<int*>(workspace);
+  hipLaunchKernelGGL(morton_count_kernel, dim3(blocks), dim3(kMortonThreads), 0, (hipStream_t)stream, *s, bits / 2,
+                     n_rays, n_idx, counts);
+  hipLaunchKernelGGL(morton_emit_kernel, dim3(blocks), dim3(kMortonThreads), 0, (hipStream_t)stream, *s, image, c2w,
+                     bits / 2, n_rays, n_idx, counts, rays, target);
   return hip_status(hipGetLastError());
 }
 

@@ -323,11 +323,16 @@ class RenderRaysFn(torch.autograd.Function):
 # --------------------------------------------------------------------------
 # training-step driver (run_nerf.py:576-636)
 # --------------------------------------------------------------------------
-def sample_rays(image, c2w, n_rays, K, near, far, crop, seed):
+def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1):
     """N_rand distinct pixels of one image (device, no replacement) -> the
     [n, 11] ray batch render() builds and the [n, 3] target colours.
     image [H, W, 3], c2w [3, 4] (or [4, 4]) fp32 on the device; crop =
-    (y0, x0, h, w) sampling window; K the 3x3 intrinsics (host numbers)."""
+    (y0, x0, h, w) sampling window; K the 3x3 intrinsics (host numbers).
+    order=1 (hn_sample_rays_morton) lists the same drawn set in Morton order
+    of its pixels -- the batch order changes the loss and its gradient only
+    by float summation order -- so the fused forward's XCD-contiguous ray
+    groups are spatially coherent; order=0 (hn_sample_rays) keeps the draw
+    order.  Both are deterministic for a given seed."""
     L.require_device(image, c2w)
     image, c2w = image.contiguous(), c2w[:3, :4].contiguous()
     H, W = image.shape[0], image.shape[1]
@@ -340,9 +345,31 @@ def sample_rays(image, c2w, n_rays, K, near, far, crop, seed):
     dev = image.device
     rays = torch.empty((n_rays, 11), dtype=torch.float32, device=dev)
     target = torch.empty((n_rays, 3), dtype=torch.float32, device=dev)
-    L.check(L.lib().hn_sample_rays(s, L.ptr(image), L.ptr(c2w), n_rays, L.ptr(rays), L.ptr(target),
-                                   L.stream(dev)), "sample_rays")
+    if order == 1:
+        nb = L.lib().hn_sample_rays_morton_workspace_bytes(s)
+        if nb == 0:
+            raise ValueError(f"sample_rays(order=1): window {s.crop_h}x{s.crop_w} too large")
+        ws = _sampler_ws(dev, nb)
+        L.check(L.lib().hn_sample_rays_morton(s, L.ptr(image), L.ptr(c2w), n_rays, L.ptr(rays), L.ptr(target),
+                                              L.ptr(ws), nb, L.stream(dev)), "sample_rays_morton")
+    elif order == 0:
+        L.check(L.lib().hn_sample_rays(s, L.ptr(image), L.ptr(c2w), n_rays, L.ptr(rays), L.ptr(target),
+                                       L.stream(dev)), "sample_rays")
+    else:
+        raise ValueError(f"sample_rays: order {order!r}")
     return rays, target
+
+
+_SAMPLER_WS = {}
+
+
+def _sampler_ws(dev, nbytes):
+    """Per-device scratch of the Morton sampler (block counts), grown on demand."""
+    ws = _SAMPLER_WS.get(dev)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _SAMPLER_WS[dev] = ws
+    return ws
 
 
 def loss_fwd(rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w):

@@ -231,12 +231,14 @@ class Trainer:
     module API with eager torch sampling and loss ops (randperm, img2mse,
     sums), the op-for-op rendition of run_nerf.py."""
 
-    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0, mode="explicit"):
+    def __init__(self, args, data: SyntheticBlender, device, rank=0, world=1, seed=0, mode="explicit",
+                 ray_order=1):
         self.args, self.data, self.device = args, data, torch.device(device)
         self.rank, self.world = rank, world
         if mode not in ("explicit", "autograd", "eager"):
             raise ValueError(f"Trainer mode {mode!r}")
         self.seed, self.mode = seed, mode
+        self.ray_order = ray_order   # functional.sample_rays order: 1 Morton (default), 0 draw order
         args.bounding_box = data.bounding_box
         torch.manual_seed(seed)                      # identical init on every rank
         (self.kw_train, self.kw_test, self.start, self.grad_vars,
@@ -322,7 +324,7 @@ class Trainer:
         img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
         crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
         rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], B, d.K, 2., 6., crop,
-                                      _step_seed(self.seed, self.rank, i))
+                                      _step_seed(self.seed, self.rank, i), order=self.ray_order)
         perturb = kw.get("perturb", 0.) > 0.
         t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
         u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
@@ -376,7 +378,7 @@ class Trainer:
                 img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
                 crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
                 rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
-                                              _step_seed(self.seed, self.rank, i))
+                                              _step_seed(self.seed, self.rank, i), order=self.ray_order)
                 rgb, depth, acc, extras = render_ray_batch(rays, (a.N_rand,), chunk=a.chunk, retraw=True,
                                                            **self.kw_train)
                 tv = None

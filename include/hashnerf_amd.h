@@ -229,6 +229,16 @@ typedef struct hn_ray_sampler {
 } hn_ray_sampler;
 int32_t hn_sample_rays(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
                        float* rays, float* target, void* stream);
+/* The same draw (same set for the same seed) listed in Morton order of its
+ * pixels (window-relative row, column), so consecutive rays are spatial
+ * neighbours: hn_render_fwd gives consecutive ray groups to one XCD and they
+ * share its L2.  Pixel x is drawn iff perm^-1(x) < n_rays, so the Morton walk
+ * of the window compacts the draw in order, without a sort.  Window sides up
+ * to HN_SAMPLER_MORTON_MAX; workspace = hn_sample_rays_morton_workspace_bytes. */
+#define HN_SAMPLER_MORTON_MAX 4096
+size_t hn_sample_rays_morton_workspace_bytes(const hn_ray_sampler* s);
+int32_t hn_sample_rays_morton(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
+                              float* rays, float* target, void* workspace, size_t ws_bytes, void* stream);
 
 /* Training loss (run_nerf.py:612-636 with the data-parallel rule of
  * SURVEY 8e): loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * (sum sp + sum sp0)
