@@ -64,6 +64,37 @@ def test_sample_rays_full_window_is_a_permutation(hn):
     assert not torch.equal(rays[:256], r2), "seed changes the sample"
 
 
+def _morton(row, col):
+    key = np.zeros_like(row)
+    for b in range(16):
+        key |= ((row >> b) & 1) << (2 * b + 1) | ((col >> b) & 1) << (2 * b)
+    return key
+
+
+@pytest.mark.parametrize("crop,n", [((0, 0, 64, 64), 1000), ((16, 8, 32, 40), 700), ((0, 0, 64, 64), 1)])
+def test_morton_sampler_same_draw_in_morton_order(hn, crop, n):
+    """order=1 (hn_sample_rays_morton) returns exactly the draw of order=0
+    (hn_sample_rays) for the same seed, listed in Morton order of the
+    window-relative (row, col), deterministically."""
+    from hashnerf_pytorch_amd import functional as HF
+    H, W, K, c2w, img = _cam(hn)
+    r0, t0 = HF.sample_rays(img, c2w, n, K, 2.0, 6.0, crop, seed=4242, order=0)
+    r1, t1 = HF.sample_rays(img, c2w, n, K, 2.0, 6.0, crop, seed=4242, order=1)
+    r1b, _ = HF.sample_rays(img, c2w, n, K, 2.0, 6.0, crop, seed=4242, order=1)
+    assert torch.equal(r1, r1b), "deterministic"
+    d_all = hn.get_rays(H, W, K, c2w)[1].reshape(-1, 3)
+    p0 = torch.cdist(r0[:, 3:6], d_all).argmin(1).cpu().numpy()
+    p1 = torch.cdist(r1[:, 3:6], d_all).argmin(1).cpu().numpy()
+    assert np.array_equal(np.sort(p0), np.sort(p1)), "same set of pixels"
+    y0, x0 = crop[0], crop[1]
+    keys = _morton(p1 // W - y0, p1 % W - x0)
+    assert np.all(np.diff(keys) > 0), "Morton order"
+    # each ray keeps its own target colour
+    order = np.argsort(p0)
+    inv = np.argsort(p1)
+    assert torch.equal(t0[torch.from_numpy(order).to(DEV)], t1[torch.from_numpy(inv).to(DEV)])
+
+
 @pytest.mark.parametrize("world,tv", [(1, False), (2, True)])
 def test_fused_loss_matches_eager(hn, world, tv):
     from hashnerf_pytorch_amd import functional as HF
