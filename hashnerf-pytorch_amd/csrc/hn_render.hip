@@ -672,8 +672,10 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 // issues a level's 4 (-1: no cap).  Uncapped, its atomics crowd the CU's
 // vector-memory pipeline and the MLP waves' weight loads stall behind them
 // (backward 1.59 ms at config 2); capped too tightly, the scatter wave waits
-// on atomic latency.  Measured (scripts/variants.sh): 1: 1.59 ms, 2: 1.56,
-// 4: 1.496, 6: 1.508.
+// on atomic latency.  Measured with the f32-MFMA MLP (scripts/variants.sh):
+// 1: 1.59 ms, 2: 1.56, 4: 1.496, 6: 1.508.  With the split-f32 MLP and
+// Morton-ordered batches (scripts/variants_env.sh, two runs each): 4: 1.282 /
+// 1.278 ms, 8: 1.258 / 1.252, 12: 1.275 / 1.274.
 #ifndef HN_NMERGE
 #define HN_NMERGE 0
 #endif
@@ -681,7 +683,7 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 #define HN_SPLIT_INSTR 0
 #endif
 #ifndef HN_SW_VMCNT
-#define HN_SW_VMCNT 4
+#define HN_SW_VMCNT 8
 #endif
 // One level of the scatter for the 16 points of a pass; v = this lane's
 // point's voxel {cell x, cell y * PY, cell z * PZ, w x, y, z} from the compact
