@@ -1177,7 +1177,13 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   static_for<0, 2>([&](auto tc) {   // unrolled: the ring's slots and the per-tile arrays stay static
     constexpr int t = decltype(tc)::value;
     if (t == 0) HN_LAP(pc, unit);
+#if HN_ABLATE == 2   // diagnostic build: no MLP backward, the scatter runs on stand-in grads
+    f32x16 dfeat = t ? featn : feat;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dfeat[r] *= dr[t].x;
+#else
     const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
+#endif
     HN_LAP(pc, mlp);
     const int qbase = 32 * (tile0 + t);
     if constexpr (fine) {
