@@ -149,10 +149,15 @@ HN_DEV void ray_sh(const Ray& r, int h, float sh8[8], float shx8[8]) {
   }
 }
 
-constexpr int kGsLds = 48;   // grid sizes [16][3] staged in LDS (saves 48 SGPRs)
+// grid sizes [16][3] staged in LDS (saves 48 SGPRs), then their reciprocals
+constexpr int kGsRcp = 48, kGsLds = 96;
 
 HN_DEV void stage_grid_sizes(const GridArgs& g, float* gsl) {
-  if (threadIdx.x < 48) gsl[threadIdx.x] = g.gs[threadIdx.x / 3][threadIdx.x % 3];
+  if (threadIdx.x < 48) {
+    const float gs = g.gs[threadIdx.x / 3][threadIdx.x % 3];
+    gsl[threadIdx.x] = gs;
+    gsl[kGsRcp + threadIdx.x] = 1.f / gs;
+  }
 }
 
 // LDS per forward wave (floats).
@@ -652,18 +657,46 @@ HN_DEV float dpp_f(float v) {
 constexpr int kRowShr1 = 0x111;              // lane i <- lane i-1 within its row
 template <int D> constexpr int kRowShl = 0x100 + D;   // lane i <- lane i+D within its row
 
-// Voxel of one (point, level): cell corner index and trilinear weights, in
-// the op order of hash_encoding.py:62-72 / :130-140 (exact IEEE divisions).
+// Voxel of one (point, level) for the scatter: cell corner index and
+// trilinear weights in the op order of hash_encoding.py:62-72 / :130-140.
+#ifndef HN_FAST_VOXEL
+#define HN_FAST_VOXEL 0
+#endif
 HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], const float xc[3], int l,
                      int32_t cell[3], float w[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const float gs = gsl[3 * l + a];
-    const float q = (xc[a] - g.bmin[a]) / gs;
+#if HN_FAST_VOXEL
+    // The cell must be the forward's: floor of the IEEE quotient (x-min)/g.
+    // (x-min) * RN(1/g) is within 2^-23 relative of it, i.e. within 1.3e-4
+    // cells for q <= 1024, so its floor is the quotient's unless the
+    // fraction lies within 2^-10 of an integer: only then (~0.2% of lanes)
+    // the IEEE division is redone.  The weights only scale the gradient:
+    // v_rcp_f32 (1 ulp) instead of the IEEE division moves them by ~2 ulp
+    // (gradient tolerance rtol 1e-4); the forward's weights stay exact.
+    // Measured: no gain (backward 1.267 ms vs 1.256 ms with the IEEE
+    // divisions): the scatter wave's VALU hides under its atomic stalls, so
+    // it stays off.
+    const float num = xc[a] - g.bmin[a];
+    float q = num * gsl[kGsRcp + 3 * l + a];
+    float fq = floorf(q);
+    const float fr = q - fq;
+    if (fr < 0x1p-10f || fr > 1.f - 0x1p-10f) {
+      q = num / gs;
+      fq = floorf(q);
+    }
+    const int32_t i = (int32_t)fq;
+    const float vmin = (float)i * gs + g.bmin[a];
+    const float vmax = vmin + gs;
+    w[a] = (pt[a] - vmin) * __builtin_amdgcn_rcpf(vmax - vmin);
+#else
+    const float q = (xc[a] - g.bmin[a]) / gs;   // exact IEEE divisions
     const int32_t i = (int32_t)floorf(q);
     const float vmin = (float)i * gs + g.bmin[a];
     const float vmax = vmin + gs;
     w[a] = (pt[a] - vmin) / (vmax - vmin);
+#endif
     cell[a] = i;
   }
 }
@@ -699,6 +732,7 @@ struct AQ {
   uint32_t head, tail;
   uint32_t nb;      // batches held in e[]
   float2 e[4];
+  uint64_t cap_wait;   // HN_PROFILE: cycles spent waiting on the in-flight cap
 };
 #ifndef HN_QCAP   // compacted atomic wave-instructions in flight before the next is issued
 #define HN_QCAP 4
@@ -862,7 +896,13 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     // cap the atomics in flight (they share the CU's vector-memory pipeline
     // with the MLP waves' weight loads); waiting only here, after this
     // level's VALU, overlaps the wait with it
+#if HN_PROFILE
+    const uint64_t tw_ = __builtin_amdgcn_s_memtime();
+#endif
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HN_SW_VMCNT) : "memory");
+#if HN_PROFILE
+    aq.cap_wait += __builtin_amdgcn_s_memtime() - tw_;
+#endif
 #endif
 #if HN_SPLIT_INSTR   // diagnostic: the same requests in twice the wave-instructions
     for (int half = 0; half < 2; ++half) {
@@ -914,7 +954,7 @@ struct PhaseClock {
 __device__ unsigned long long g_phase[2][8];
 // ring waits: [0] scatter wave total, [1] scatter wave waiting on ready,
 // [2] MLP waves waiting on a free slot, [3] MLP waves waiting on the coarse flag
-__device__ unsigned long long g_ring[4];
+__device__ unsigned long long g_ring[5];   // [4] scatter wave waiting on the atomic cap
 #else
 #define HN_LAP(pc, field) ((void)0)
 #endif
@@ -1079,7 +1119,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
       if (lane == 0) atomicAdd(q.selfc, 1);
       fill_slot(X, r, z, dfeat, tw);
       static_assert(!HN_MW_SELF || !HN_COMPACT, "the compacted queue belongs to the scatter wave");
-      AQ none{nullptr, 0u, 0u, 0u, {}};
+      AQ none{nullptr, 0u, 0u, 0u, {}, 0ull};
       scatter_slot(k, X, X + kSlotF, q.gsl, none);
       return;
     }
@@ -1099,7 +1139,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
 // only grow and a tile is counted before it is handled, so tick + selfc ==
 // n_tiles with t >= tick means no ticket t will ever come.
 HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
-  AQ aq{reinterpret_cast<float2*>(V + kVoxF), 0u, 0u, 0u, {}};
+  AQ aq{reinterpret_cast<float2*>(V + kVoxF), 0u, 0u, 0u, {}, 0ull};
   for (int t = 0;; ++t) {
     const int s = t % kSlots;
 #if HN_PROFILE
@@ -1125,6 +1165,9 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
     ring_publish(&q.freed[s], t / kSlots + 1);
   }
   if (HN_COMPACT) aq_drain(k.d_table, aq, lane_id());
+#if HN_PROFILE
+  if (lane_id() == 0) atomicAdd(&g_ring[4], (unsigned long long)aq.cap_wait);
+#endif
 }
 
 HN_DEV void wait_flag(int* flag, int need) {
@@ -1576,11 +1619,11 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
               (double)ph[f][2] / ph[f][4], (double)ph[f][3] / ph[f][4]);
     memset(ph, 0, sizeof(ph));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph));
-    unsigned long long rg[4];
+    unsigned long long rg[5];
     (void)hipMemcpyFromSymbol(rg, HIP_SYMBOL(g_ring), sizeof(rg));
-    fprintf(stderr, "hn_b1_ring per block: scatter wave total %.0f waiting %.0f | MLP waves slot-wait %.0f "
-            "coarse-wait %.0f (per wave)\n", rg[0] / 256., rg[1] / 256., rg[2] / (256. * kMW),
-            rg[3] / (256. * kMW));
+    fprintf(stderr, "hn_b1_ring per block: scatter wave total %.0f waiting %.0f cap-wait %.0f | MLP waves "
+            "slot-wait %.0f coarse-wait %.0f (per wave)\n", rg[0] / 256., rg[1] / 256., rg[4] / 256.,
+            rg[2] / (256. * kMW), rg[3] / (256. * kMW));
     memset(rg, 0, sizeof(rg));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ring), rg, sizeof(rg));
   }
