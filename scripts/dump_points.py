@@ -17,8 +17,10 @@ from hashnerf_pytorch_amd.render import render_ray_batch  # noqa: E402
 from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args  # noqa: E402
 
 dev = torch.device("cuda")
+# usage: python scripts/dump_points.py [train_steps] [scene: uniform | procedural]
 args = default_args(N_rand=4096, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6, tv_until=10 ** 9)
-data = SyntheticBlender(400, 400, 100, dev, seed=0)
+scene = sys.argv[2] if len(sys.argv) > 2 else "uniform"
+data = SyntheticBlender(400, 400, 100, dev, seed=0, scene=scene)
 tr = Trainer(args, data, dev)
 for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 10):
     tr.step(i)
