@@ -364,7 +364,21 @@ constexpr int kB1Img = kMW * kRRows * kXS;                 // floats (112,320 B)
 #endif
 constexpr int kSlots = HN_SLOTS;
 constexpr int kSlotZ = 32 * kXS, kSlotR = kSlotZ + 32, kSlotF = kSlotR + 8;
-constexpr int kVoxF = 16 * 16 * 8;                         // scatter wave's voxel buffer
+// Tile-span runs (HN_TILE_RUNS, scatter_slot): a run of samples in one voxel
+// that crosses from a tile's first 16-point group into its second is issued
+// once, with the second group.  Needs the second group's first cell per
+// level and the held run's values: [16 levels][4] + [16 levels][4 rows][4].
+// Measured off (config 2, procedural after 1000 steps): memory-side atomic
+// requests -5.4 % (20.26 M -> 19.16 M per launch, as scripts/
+// request_model_runs.py predicts) but the backward 1.25 -> 1.32 ms, for any
+// in-flight cap 4..12; the carry's own work without its merges
+// (HN_TILE_RUNS_OFF) costs ~0.01 ms.  The slowdown comes from the merged
+// issue pattern itself, not from the added instructions.
+#ifndef HN_TILE_RUNS
+#define HN_TILE_RUNS 0
+#endif
+constexpr int kCarryF = HN_TILE_RUNS ? 16 * 4 + 16 * 16 : 0;
+constexpr int kVoxF = 16 * 16 * 8 + kCarryF;               // scatter wave's voxel buffer (+ run carry)
 // Compacted atomic issue (HN_COMPACT, scatter_level_x): a ring of kQ {byte
 // offset, value} slots right after the voxel buffer.
 #ifndef HN_COMPACT
@@ -773,7 +787,9 @@ HN_DEV void aq_drain(float* __restrict__ dtable, AQ& q, int lane) {
 }
 
 HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const f32x4 v0, const float2 v1,
-                            uint32_t l, float gl, int lane, AQ& aq) {
+                            uint32_t l, float gl, int lane, AQ& aq, [[maybe_unused]] bool hold = false,
+                            [[maybe_unused]] bool take = false, [[maybe_unused]] f32x4 carry_in = {},
+                            [[maybe_unused]] float* carry_out = nullptr) {
   const int pp = lane & 15, xi = lane >> 5;
   [[maybe_unused]] const int f = (lane >> 4) & 1;
   const uint32_t cx = (uint32_t)__float_as_int(v0.x), y0 = (uint32_t)__float_as_int(v0.y),
@@ -818,6 +834,21 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     }
   };
   seg_sum(cv);
+  bool issue = head;
+#if HN_TILE_RUNS
+  // take: this group's first run continues the previous group's last one,
+  // whose sums (rows c = 0..3 of this lane's x/feature) arrive in carry_in;
+  // hold: this group's last run continues into the next group, so its head
+  // parks its sums at carry_out instead of issuing them
+  static_assert(!HN_NMERGE && !HN_COMPACT, "the tile-span carry is wired into the row-per-instruction scatter only");
+  if (take && pp == 0) {
+    cv[0] += carry_in.x; cv[1] += carry_in.y; cv[2] += carry_in.z; cv[3] += carry_in.w;
+  }
+  if (hold && pp == 31 - __builtin_clz(pm)) {
+    *reinterpret_cast<f32x4*>(carry_out) = f32x4{cv[0], cv[1], cv[2], cv[3]};
+    issue = false;
+  }
+#endif
   // Neighbour merge: consecutive run heads along the ray are usually
   // adjacent voxels.  After a y/z step a head shares the corner rows (register
   // c = 2j+k, both x lanes) of the common face with the previous head.  Heads
@@ -888,7 +919,7 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     aq_read(aq, lane);
   }
 #else
-  if (head) {
+  if (issue) {
     const uint32_t row0 = l << g.log2T;
     const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
                             (hx ^ y1 ^ z1) & mask};
@@ -1045,6 +1076,7 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
     r.o[a] = S[kSlotR + a];
     r.d[a] = S[kSlotR + 3 + a];
   }
+  [[maybe_unused]] uint32_t cont = 0u;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
     float pt[3], xc[3];
@@ -1065,7 +1097,35 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
                                               __uint_as_float((uint32_t)cell[2] * kPrimeZ), w[0]};
       *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
     }
+#if HN_TILE_RUNS
+    float* const cc = V + 16 * 16 * 8;          // [level][cx, cy*PY, cz*PZ, -]: group 1's first point
+    if (grp == 0 && lane < 16) {                // lane = level
+      float p16[3], x16[3];
+      ray_point(r, S[kSlotZ + 16], p16);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) x16[a] = clamp_t(p16[a], k.g.bmin[a], k.g.bmax[a]);
+      int32_t cell[3];
+      float w[3];
+      voxel_cw(k.g, gsl, p16, x16, lane, cell, w);
+      *reinterpret_cast<f32x4*>(cc + 4 * lane) =
+          f32x4{__int_as_float(cell[0]), __uint_as_float((uint32_t)cell[1] * kPrimeY),
+                __uint_as_float((uint32_t)cell[2] * kPrimeZ), 0.f};
+    }
+#endif
     lds_fence_wave();
+#if HN_TILE_RUNS
+    if (grp == 0) {                             // bit l: group 0's last cell at level l == group 1's first
+      const int li = lane & 15;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(V + (li * 16 + 15) * 8);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(cc + 4 * li);
+      const bool eq = __float_as_uint(a.x) == __float_as_uint(b.x) && __float_as_uint(a.y) == __float_as_uint(b.y) &&
+                      __float_as_uint(a.z) == __float_as_uint(b.z);
+      cont = (uint32_t)__ballot(eq) & 0xffffu;
+#ifdef HN_TILE_RUNS_OFF   // diagnostic: the carry's overhead without its merges
+      cont = 0u;
+#endif
+    }
+#endif
     float gl[16];
     const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + 16 * f);
 #pragma unroll
@@ -1078,15 +1138,32 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
     const float* vs = V + pp * 8;
     f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
     float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
+#if HN_TILE_RUNS
+    // held sums [level][lane-in-unit][row], read one level ahead like the records
+    float* const cs = V + 16 * 16 * 8 + 64 + 4 * (lane >> 4);
+    f32x4 cr = grp ? *reinterpret_cast<const f32x4*>(cs) : f32x4{};
+#endif
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
       const f32x4 c0 = v0;
       const float2 c1 = v1;
+#if HN_TILE_RUNS
+      const f32x4 cc0 = cr;
+#endif
       if (l < 15) {
         v0 = *reinterpret_cast<const f32x4*>(vs + (l + 1) * 128);
         v1 = *reinterpret_cast<const float2*>(vs + (l + 1) * 128 + 4);
+#if HN_TILE_RUNS
+        if (grp) cr = *reinterpret_cast<const f32x4*>(cs + 16 * (l + 1));
+#endif
       }
+#if HN_TILE_RUNS
+      const bool cl = (cont >> l) & 1u;
+      scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane, aq, cl && grp == 0, cl && grp == 1, cc0,
+                      cs + 16 * l);
+#else
       scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
+#endif
       if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
