@@ -919,10 +919,19 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     aq_read(aq, lane);
   }
 #else
+#ifdef HN_SKIP_LEVELS   // diagnostic: no atomics for the levels in this mask (wrong gradients)
+  if ((HN_SKIP_LEVELS >> l) & 1u) issue = false;
+#endif
   if (issue) {
     const uint32_t row0 = l << g.log2T;
+#ifdef HN_DIAG_REP   // diagnostic: levels < HN_DIAG_REP spread over 8 row-shifted copies (wrong gradients)
+    const uint32_t sh_ = l < HN_DIAG_REP ? (blockIdx.x & 7u) << 16 : 0u;
+    const uint32_t hh[4] = {((hx ^ y0 ^ z0) + sh_) & mask, ((hx ^ y0 ^ z1) + sh_) & mask,
+                            ((hx ^ y1 ^ z0) + sh_) & mask, ((hx ^ y1 ^ z1) + sh_) & mask};
+#else
     const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
                             (hx ^ y1 ^ z1) & mask};
+#endif
 #if HN_SW_VMCNT >= 0
     // cap the atomics in flight (they share the CU's vector-memory pipeline
     // with the MLP waves' weight loads); waiting only here, after this
