@@ -11,6 +11,11 @@ namespace hn {
 struct TvK {
   int32_t L, log2T;
   int32_t cube[HN_MAX_LEVELS];
+  // packed 1-D grids: level l owns blocks [boff[l], boff[l+1]) of the
+  // forward (kTvFwdV vertices per thread) and [bofb[l], bofb[l+1]) of the
+  // backward (one thread per (vertex, feature)), instead of a (max blocks) x L
+  // grid that is mostly idle blocks
+  int32_t boff[HN_MAX_LEVELS + 1], bofb[HN_MAX_LEVELS + 1];
   const int32_t* mv;
   const float* table;
 };
@@ -30,23 +35,40 @@ HN_DEV float block_sum_256(float v) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// level of packed block b (wave-uniform; at most 16 scalar compares)
+HN_DEV int tv_level(const TvK& k, const int32_t* off, int b) {
+  int l = 0;
+  while (l + 1 < k.L && b >= off[l + 1]) ++l;
+  return l;
+}
+
+// vertices per forward thread: fewer blocks, so fewer same-address atomics
+// on the 16 level sums
+#ifndef HN_TV_FWD_V
+#define HN_TV_FWD_V 4
+#endif
+constexpr int kTvFwdV = HN_TV_FWD_V;
+
 __global__ __launch_bounds__(256) void tv_fwd_kernel(TvK k, float* __restrict__ tv) {
-  const int l = blockIdx.y;
+  const int l = tv_level(k, k.boff, blockIdx.x);
   const int c = k.cube[l], n1 = c + 1;
-  const int t = blockIdx.x * 256 + threadIdx.x;
   float acc = 0.f;
-  if (t < n1 * n1 * n1) {
-    // x fastest across the lanes: h(x..x+7) of one (y, z) fill one 64-B
-    // segment, so neighbouring lanes' gathers share cache lines (the TV sum is
-    // order-free up to fp32 rounding; the reference's 'ij' order is only its
-    // summation order)
-    const int i = t % n1, j = (t / n1) % n1, kk = t / (n1 * n1);
-    const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
-                   z = (uint32_t)(k.mv[3 * l + 2] + kk);
-    const float2 e = tv_row(k, l, x, y, z);
-    if (i < c) { const float2 n = tv_row(k, l, x + 1, y, z); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
-    if (j < c) { const float2 n = tv_row(k, l, x, y + 1, z); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
-    if (kk < c) { const float2 n = tv_row(k, l, x, y, z + 1); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+#pragma unroll
+  for (int q = 0; q < kTvFwdV; ++q) {
+    const int t = ((blockIdx.x - k.boff[l]) * kTvFwdV + q) * 256 + threadIdx.x;
+    if (t < n1 * n1 * n1) {
+      // x fastest across the lanes: h(x..x+7) of one (y, z) fill one 64-B
+      // segment, so neighbouring lanes' gathers share cache lines (the TV sum is
+      // order-free up to fp32 rounding; the reference's 'ij' order is only its
+      // summation order)
+      const int i = t % n1, j = (t / n1) % n1, kk = t / (n1 * n1);
+      const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
+                     z = (uint32_t)(k.mv[3 * l + 2] + kk);
+      const float2 e = tv_row(k, l, x, y, z);
+      if (i < c) { const float2 n = tv_row(k, l, x + 1, y, z); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+      if (j < c) { const float2 n = tv_row(k, l, x, y + 1, z); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+      if (kk < c) { const float2 n = tv_row(k, l, x, y, z + 1); const float a = n.x - e.x, b = n.y - e.y; acc += a * a + b * b; }
+    }
   }
   const float s = block_sum_256(acc);
   if (threadIdx.x == 0 && s != 0.f) atomic_add_f32(tv + l, s / (float)c);
@@ -63,9 +85,9 @@ HN_DEV float tv_val(const TvK& k, int l, uint32_t x, uint32_t y, uint32_t z, int
 
 __global__ __launch_bounds__(256) void tv_bwd_kernel(TvK k, const float* __restrict__ g_tv,
                                                      float* __restrict__ dtable) {
-  const int l = blockIdx.y;
+  const int l = tv_level(k, k.bofb, blockIdx.x);
   const int c = k.cube[l], n1 = c + 1;
-  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int t = (blockIdx.x - k.bofb[l]) * 256 + threadIdx.x;
   const int v = t >> 1, f = t & 1;
   if (v >= n1 * n1 * n1) return;
   const int i = v % n1, j = (v / n1) % n1, kk = v / (n1 * n1);
@@ -135,7 +157,7 @@ __global__ __launch_bounds__(256) void radam_kernel(RadamK k) {
   }
 }
 
-static int32_t make_tv(const hn_tv_args* a, TvK& k, int& max_blocks) {
+static int32_t make_tv(const hn_tv_args* a, TvK& k, int& fwd_blocks, int& bwd_blocks) {
   if (!a || !a->min_vertex || !a->table) return HN_E_NULL;
   if (a->n_levels < 1 || a->n_levels > HN_MAX_LEVELS) return HN_E_SHAPE;
   if (a->log2_hashmap_size < 1 || a->log2_hashmap_size > 24) return HN_E_SHAPE;
@@ -143,14 +165,20 @@ static int32_t make_tv(const hn_tv_args* a, TvK& k, int& max_blocks) {
   k.log2T = a->log2_hashmap_size;
   k.mv = a->min_vertex;
   k.table = a->table;
-  max_blocks = 1;
   for (int l = 0; l < HN_MAX_LEVELS; ++l) k.cube[l] = l < a->n_levels ? a->cube[l] : 1;
-  for (int l = 0; l < a->n_levels; ++l) {
-    const int c = a->cube[l];
-    if (c < 1 || c > 1000) return HN_E_SHAPE;
-    const int nb = ((c + 1) * (c + 1) * (c + 1) + 255) / 256;
-    max_blocks = nb > max_blocks ? nb : max_blocks;
+  k.boff[0] = k.bofb[0] = 0;
+  for (int l = 0; l < HN_MAX_LEVELS; ++l) {
+    int nv = 0;
+    if (l < a->n_levels) {
+      const int c = a->cube[l];
+      if (c < 1 || c > 1000) return HN_E_SHAPE;
+      nv = (c + 1) * (c + 1) * (c + 1);
+    }
+    k.boff[l + 1] = k.boff[l] + (nv + 256 * kTvFwdV - 1) / (256 * kTvFwdV);
+    k.bofb[l + 1] = k.bofb[l] + (2 * nv + 255) / 256;
   }
+  fwd_blocks = k.boff[a->n_levels];
+  bwd_blocks = k.bofb[a->n_levels];
   return HN_OK;
 }
 
@@ -160,23 +188,23 @@ using namespace hn;
 
 extern "C" int32_t hn_tv_fwd(const hn_tv_args* a, float* tv, void* stream) {
   TvK k;
-  int nb;
-  int32_t st = make_tv(a, k, nb);
+  int nb, nbb;
+  int32_t st = make_tv(a, k, nb, nbb);
   if (st) return st;
   if (!tv) return HN_E_NULL;
   hipStream_t s = (hipStream_t)stream;
   if ((st = hip_status(hipMemsetAsync(tv, 0, sizeof(float) * a->n_levels, s)))) return st;
-  hipLaunchKernelGGL(tv_fwd_kernel, dim3(nb, a->n_levels), dim3(256), 0, s, k, tv);
+  hipLaunchKernelGGL(tv_fwd_kernel, dim3(nb), dim3(256), 0, s, k, tv);
   return hip_status(hipGetLastError());
 }
 
 extern "C" int32_t hn_tv_bwd(const hn_tv_args* a, const float* g_tv, float* dtable, void* stream) {
   TvK k;
-  int nb;
-  int32_t st = make_tv(a, k, nb);
+  int nb, nbb;
+  int32_t st = make_tv(a, k, nb, nbb);
   if (st) return st;
   if (!g_tv || !dtable) return HN_E_NULL;
-  hipLaunchKernelGGL(tv_bwd_kernel, dim3(2 * nb, a->n_levels), dim3(256), 0, (hipStream_t)stream, k, g_tv,
+  hipLaunchKernelGGL(tv_bwd_kernel, dim3(nbb), dim3(256), 0, (hipStream_t)stream, k, g_tv,
                      dtable);
   return hip_status(hipGetLastError());
 }
