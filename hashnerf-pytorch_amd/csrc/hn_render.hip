@@ -1536,27 +1536,38 @@ void render_bwd_kernel(B1K k) {
 }
 
 // dW(coarse) += sum_b slab[b][0], dW(fine) += sum_b slab[b][1].  64
-// consecutive elements per block, 4 block-groups per element, LDS combine.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs,
-                                                          hn_mlp_grad dc, hn_mlp_grad df) {
-  __shared__ float part[4][64];
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+// consecutive elements per block, kSlabGroups slab-groups per element (8
+// loads in flight per thread, ~18 waves per CU: the 19 MB read is latency
+// bound otherwise), LDS combine in a fixed order, so the sums are
+// deterministic.
+constexpr int kSlabGroups = 16;
+__global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs,
+                                                                       hn_mlp_grad dc, hn_mlp_grad df) {
+  __shared__ float part[kSlabGroups][64];
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 64 + lane;
   const int grp = threadIdx.x >> 6;
   float s = 0.f;
   if (e < 2 * W_END) {
-    // four independent chains keep 4 loads in flight per thread
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int b = grp;
-    for (; b + 12 < n_slabs; b += 16)
+    for (; b + 7 * kSlabGroups < n_slabs; b += 8 * kSlabGroups)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] += slab[(size_t)(b + 4 * q) * 2 * W_END + e];
-    for (; b < n_slabs; b += 4) acc[0] += slab[(size_t)b * 2 * W_END + e];
-    s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      for (int q = 0; q < 8; ++q) acc[q] += slab[(size_t)(b + kSlabGroups * q) * 2 * W_END + e];
+    for (; b < n_slabs; b += kSlabGroups) acc[0] += slab[(size_t)b * 2 * W_END + e];
+    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
-  part[grp][threadIdx.x & 63] = s;
+  part[grp][lane] = s;
   __syncthreads();
   if (grp != 0 || e >= 2 * W_END) return;
-  s = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+  float t[kSlabGroups];
+#pragma unroll
+  for (int g = 0; g < kSlabGroups; ++g) t[g] = part[g][lane];
+#pragma unroll
+  for (int w = kSlabGroups / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int g = 0; g < w; ++g) t[g] = t[g] + t[g + w];
+  s = t[0];
   const bool fine = e >= W_END;
   const int i = fine ? e - W_END : e;
   const hn_mlp_grad& d = fine ? df : dc;
@@ -1714,7 +1725,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ring), rg, sizeof(rg));
   }
 #endif
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(256), 0, s, slab, kBwdBlocks,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,
                      a->d_coarse, a->d_fine);
   return hip_status(hipGetLastError());
 }
