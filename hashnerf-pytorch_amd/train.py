@@ -326,15 +326,9 @@ class Trainer:
         rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], B, d.K, 2., 6., crop,
                                       _step_seed(self.seed, self.rank, i), order=self.ray_order)
         perturb = kw.get("perturb", 0.) > 0.
-        ns, ni = kw["N_samples"], kw["N_importance"]
-        if perturb:
-            # one RNG launch for both: the jitter and the uniforms are
-            # contiguous [B, ns] and [B, ni] views of one draw
-            r = torch.rand(B * (ns + ni), device=self.device)
-            t_rand, u = r[:B * ns].view(B, ns), r[B * ns:].view(B, ni)
-        else:
-            t_rand = None
-            u = torch.linspace(0., 1., ni, device=self.device).expand(B, ni)
+        t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
+        u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
+             torch.linspace(0., 1., kw["N_importance"], device=self.device).expand(B, kw["N_importance"]))
         tv = None
         if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
             tv = draw_tv_cubes(self.embed_fn.n_levels, self.embed_fn.base_resolution,
