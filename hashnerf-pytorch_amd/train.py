@@ -326,6 +326,9 @@ class Trainer:
         rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], B, d.K, 2., 6., crop,
                                       _step_seed(self.seed, self.rank, i), order=self.ray_order)
         perturb = kw.get("perturb", 0.) > 0.
+        # two draws in render_rays' order (run_nerf_helpers.py:528, then :276 via :548): the
+        # autograd and reference-path modes draw them the same way, so all
+        # modes see the same numbers for the same device RNG state
         t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
         u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
              torch.linspace(0., 1., kw["N_importance"], device=self.device).expand(B, kw["N_importance"]))
