@@ -732,6 +732,11 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 #ifndef HN_SW_VMCNT
 #define HN_SW_VMCNT 8
 #endif
+// The cap when the table does not fit the 256 MiB MALL (T >= 21): config 3
+// (T=22, B=8192) measured 2.93 / 2.94 ms at cap 8 and 2.82 / 2.82 ms at 4.
+#ifndef HN_SW_VMCNT_BIG
+#define HN_SW_VMCNT_BIG 4
+#endif
 // One level of the scatter for the 16 points of a pass; v = this lane's
 // point's voxel {cell x, cell y * PY, cell z * PZ, w x, y, z} from the compact
 // pass (the prime products are precomputed there: (c + 1) * P = c * P + P,
@@ -786,8 +791,10 @@ HN_DEV void aq_drain(float* __restrict__ dtable, AQ& q, int lane) {
   }
 }
 
+template <int CAP>   // in-flight atomic cap: HN_SW_VMCNT, or HN_SW_VMCNT_BIG for a table beyond the MALL
 HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const f32x4 v0, const float2 v1,
-                            uint32_t l, float gl, int lane, AQ& aq, [[maybe_unused]] bool hold = false,
+                            uint32_t l, float gl, int lane, AQ& aq,
+                            [[maybe_unused]] bool hold = false,
                             [[maybe_unused]] bool take = false, [[maybe_unused]] f32x4 carry_in = {},
                             [[maybe_unused]] float* carry_out = nullptr) {
   const int pp = lane & 15, xi = lane >> 5;
@@ -939,7 +946,7 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
 #if HN_PROFILE
     const uint64_t tw_ = __builtin_amdgcn_s_memtime();
 #endif
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HN_SW_VMCNT) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CAP) : "memory");
 #if HN_PROFILE
     aq.cap_wait += __builtin_amdgcn_s_memtime() - tw_;
 #endif
@@ -1076,6 +1083,7 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 
 // The table-gradient scatter of one slot (embedding_dense_backward of
 // hash_encoding.py:106 + trilinear backward); V = 2048-float voxel buffer.
+template <int CAP>
 HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl, AQ& aq) {
   const int lane = lane_id();
   const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
@@ -1168,10 +1176,10 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
       }
 #if HN_TILE_RUNS
       const bool cl = (cont >> l) & 1u;
-      scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane, aq, cl && grp == 0, cl && grp == 1, cc0,
+      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq, cl && grp == 0, cl && grp == 1, cc0,
                       cs + 16 * l);
 #else
-      scatter_level_x(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
+      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
 #endif
       if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
@@ -1206,7 +1214,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
       fill_slot(X, r, z, dfeat, tw);
       static_assert(!HN_MW_SELF || !HN_COMPACT, "the compacted queue belongs to the scatter wave");
       AQ none{nullptr, 0u, 0u, 0u, {}, 0ull};
-      scatter_slot(k, X, X + kSlotF, q.gsl, none);
+      scatter_slot<HN_SW_VMCNT>(k, X, X + kSlotF, q.gsl, none);
       return;
     }
   }
@@ -1224,6 +1232,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
 // is accounted for (a ticket, or scattered by its MLP wave).  tick and selfc
 // only grow and a tile is counted before it is handled, so tick + selfc ==
 // n_tiles with t >= tick means no ticket t will ever come.
+template <int CAP>
 HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
   AQ aq{reinterpret_cast<float2*>(V + kVoxF), 0u, 0u, 0u, {}, 0ull};
   for (int t = 0;; ++t) {
@@ -1247,7 +1256,7 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
 #endif
     if (!have) break;
     const float* S = q.slots + s * kSlotF;
-    scatter_slot(k, S, V, q.gsl, aq);
+    scatter_slot<CAP>(k, S, V, q.gsl, aq);
     ring_publish(&q.freed[s], t / kSlots + 1);
   }
   if (HN_COMPACT) aq_drain(k.d_table, aq, lane_id());
@@ -1443,6 +1452,7 @@ HN_DEV void dw_zero(DW& dw) {
 // wave 3 through the LDS ring; wave 3 only scatters (the table gradient is
 // bound by the memory-side float-atomic rate, so the MLP work runs under it).
 // Every wave that waits, waits on a wave of its own workgroup: co-resident.
+template <int CAP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void render_bwd_kernel(B1K k) {
   extern __shared__ f32x4 smem4[];
@@ -1487,7 +1497,7 @@ void render_bwd_kernel(B1K k) {
   const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #endif
   if (wave == kMW) {
-    ring_drain(k, ring, V, 2 * kSf / 64 * n_rays);
+    ring_drain<CAP>(k, ring, V, 2 * kSf / 64 * n_rays);
 #if HN_PROFILE
     if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
 #endif
@@ -1703,7 +1713,11 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
                      dim3(64 * kFwdWaves), 0, s, k);
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
-  hipLaunchKernelGGL(render_bwd_kernel, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
+  // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
+  if (cfg->grid.log2_hashmap_size >= 21)
+    hipLaunchKernelGGL(render_bwd_kernel<HN_SW_VMCNT_BIG>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
+  else
+    hipLaunchKernelGGL(render_bwd_kernel<HN_SW_VMCNT>, dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s, k);
   if ((st = hip_status(hipGetLastError()))) return st;
 #if HN_PROFILE
   {
