@@ -38,7 +38,7 @@ for f in sorted(glob.glob(f"{out}/pmc_{tag}_*/**/*counter_collection.csv", recur
         name = r.get("Kernel_Name", r.get("Kernel-Name", ""))
         if "hn::" not in name:
             continue
-        key = name.split("(")[0].replace("void ", "")
+        key = name.split("(")[0].split("<")[0].replace("void ", "")   # render_bwd_kernel<CAP> -> one key
         did = int(r.get("Dispatch_Id", r.get("Dispatch-Id", 0)) or 0)
         raw[key][r["Counter_Name"]].append((did, float(r["Counter_Value"])))
 agg = collections.defaultdict(dict)
