@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 3                 # HN_ABI_VERSION
+ABI_VERSION = 4                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -93,6 +93,7 @@ class HnRadamTensor(C.Structure):
 SIGNATURES = {
     "hn_abi_version": (C.c_int32, []),
     "hn_status_string": (C.c_char_p, [C.c_int32]),
+    "hn_device_faults": (C.c_int32, [C.POINTER(C.c_int32), C.c_int32]),
     "hn_encode_fwd": (C.c_int32, [C.POINTER(HnGrid), _P, C.c_int64, _P, _P, _P, _P]),
     "hn_encode_bwd": (C.c_int32, [C.POINTER(HnGrid), _P, C.c_int64, _P, _P, _P]),
     "hn_sh_fwd": (C.c_int32, [_P, C.c_int64, _P, _P]),
@@ -145,6 +146,21 @@ def check(status: int, what: str):
     if status != 0:
         msg = lib().hn_status_string(status).decode()
         raise RuntimeError(f"hashnerf_amd.{what} failed: {msg} (status {status})")
+
+
+FAULT_BITS = {1: "ring slot wait", 2: "ring drain (tiles left unscattered)", 4: "coarse-grad flag wait",
+              8: "dW buffer wait"}
+
+
+def check_device_faults(clear: bool = True):
+    """Raise if a kernel reported a failed bounded wait since the last clear
+    (hn_device_faults; synchronises the device)."""
+    w = C.c_int32(0)
+    check(lib().hn_device_faults(C.byref(w), int(clear)), "device_faults")
+    if w.value:
+        what = ", ".join(v for k, v in FAULT_BITS.items() if w.value & k) or str(w.value)
+        raise RuntimeError(f"hashnerf_amd: the render backward reported a failed internal wait ({what}); "
+                           "the gradients of the launches since the last check are invalid")
 
 
 def ptr(t: Optional[torch.Tensor]):

@@ -1026,18 +1026,32 @@ struct Ring {
   const float* gsl;
 };
 
-// Bounded spin on a workgroup-local flag (a protocol bug ends in wrong
-// results, never in a hung GPU).
-HN_DEV void spin_until(int* flag, int need, int prof_slot = -1) {
+// Sticky device fault word (hn_device_faults): a bounded wait that runs out
+// sets its bit, so a protocol bug ends in an error the host sees, never in a
+// hung GPU or in silently partial gradients.
+__device__ int g_hn_fault;
+enum : int { kFaultSlot = 1, kFaultDrain = 2, kFaultCoarse = 4, kFaultDwBuf = 8 };
+constexpr int kSpinCap = 1 << 22;   // iterations of >= 128 cycles: ~0.25 s
+HN_DEV void raise_fault(int bit) {
+  if (lane_id() == 0) __hip_atomic_fetch_or(&g_hn_fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bounded spin on a workgroup-local flag.
+HN_DEV void spin_until(int* flag, int need, int fault_bit, int prof_slot = -1) {
 #if HN_PROFILE
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-  for (int it = 0; it < (1 << 22); ++it) {
+  bool ok = false;
+  for (int it = 0; it < kSpinCap; ++it) {
     const int v = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (v >= need) break;
+    if (v >= need) {
+      ok = true;
+      break;
+    }
     __builtin_amdgcn_s_sleep(2);
   }
+  if (!ok) raise_fault(fault_bit);
   asm volatile("" ::: "memory");
 #if HN_PROFILE
   if (prof_slot >= 0 && lane_id() == 0)
@@ -1222,7 +1236,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
   if (lane == 0) t = atomicAdd(q.tick, 1);
   t = __builtin_amdgcn_readfirstlane(t);
   const int s = t % kSlots;
-  spin_until(&q.freed[s], t / kSlots, 2);
+  spin_until(&q.freed[s], t / kSlots, kFaultSlot, 2);
   float* S = q.slots + s * kSlotF;
   fill_slot(S, r, z, dfeat, tw);
   ring_publish(&q.ready[s], t + 1);
@@ -1240,16 +1254,20 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
 #if HN_PROFILE
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-    bool have = false;
-    for (int it = 0; it < (1 << 22); ++it) {
+    bool have = false, done = false;
+    for (int it = 0; it < kSpinCap; ++it) {
       if (lds_load(&q.ready[s]) >= t + 1) {
         have = true;
         break;
       }
       const int tk = lds_load(q.tick);
-      if (tk + lds_load(q.selfc) >= n_tiles && t >= tk) break;
+      if (tk + lds_load(q.selfc) >= n_tiles && t >= tk) {
+        done = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(2);
     }
+    if (!have && !done) raise_fault(kFaultDrain);   // tiles left unscattered
     asm volatile("" ::: "memory");
 #if HN_PROFILE
     if (lane_id() == 0) atomicAdd(&g_ring[1], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
@@ -1266,8 +1284,11 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
 }
 
 HN_DEV void wait_flag(int* flag, int need) {
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+  for (int it = 0; it < kSpinCap; ++it) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) return;
     __builtin_amdgcn_s_sleep(8);
+  }
+  raise_fault(kFaultCoarse);
 }
 
 // One work unit: composite backward of the ray (:541/:558 chain), then 2 tiles.
@@ -1527,7 +1548,7 @@ void render_bwd_kernel(B1K k) {
       for (int j = lane; j < W_END; j += 64) smem[j] = 0.f;
       ring_publish(&sync[3], 1);
     }
-    spin_until(&sync[3], 1);
+    spin_until(&sync[3], 1, kFaultDwBuf);
     dw_flush<false>(dw, smem, lane);
   }
 #if HN_PROFILE
@@ -1615,6 +1636,14 @@ extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   return ((size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32 + n * (kSc + kSf) * 4) *
          sizeof(float);
+}
+
+extern "C" int32_t hn_device_faults(int32_t* faults, int32_t clear) {
+  if (!faults) return HN_E_NULL;
+  int32_t st = hip_status(hipMemcpyFromSymbol(faults, HIP_SYMBOL(g_hn_fault), sizeof(int32_t)));
+  if (st || !clear || *faults == 0) return st;
+  const int32_t zero = 0;
+  return hip_status(hipMemcpyToSymbol(HIP_SYMBOL(g_hn_fault), &zero, sizeof(int32_t)));
 }
 
 extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,

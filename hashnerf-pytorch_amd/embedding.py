@@ -87,6 +87,9 @@ class HashEmbedder(nn.Module):
         self.table = nn.Parameter(torch.empty(n_levels, 2 ** log2_hashmap_size,
                                               n_features_per_level))
         nn.init.uniform_(self.table, a=-0.0001, b=0.0001)            # :55-56
+        # RAdam.state_dict / load_state_dict list this parameter as the
+        # reference's n_levels per-level embedding weights
+        self.table._hn_levels = n_levels
         self.embeddings = nn.ModuleList([_LevelEmbedding(self, l) for l in range(n_levels)])
         self._grid = None
 

@@ -7,6 +7,7 @@ the kernels, mirroring the C ABI contract.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -50,6 +51,10 @@ TIMER = KernelTimer()
 # z-values / raw outputs of the last call in LAST (no effect on results).
 DEBUG_KEEP = False
 LAST = {}
+# When True, every render backward is followed by a check of the device fault
+# word (hn_device_faults: a blocking read).  The tests turn it on; trainers
+# check every Trainer.fault_check_every steps instead.
+CHECK_FAULTS = os.environ.get("HN_CHECK_FAULTS", "0") == "1"
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
@@ -277,6 +282,8 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws):
     t0 = TIMER.begin("render_bwd")
     L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
     TIMER.end("render_bwd", t0)
+    if CHECK_FAULTS:
+        L.check_device_faults()
 
 
 def zeros_like_all(ts):

@@ -85,3 +85,84 @@ class RAdam(Optimizer):
         if work:
             HF.radam_step(work)
         return loss
+
+    # -- reference-compatible state dict --------------------------------------
+    # The reference's embedding group holds the 16 per-level nn.Embedding
+    # weights (run_nerf_helpers.py:61-62, :132-135); here it holds ONE stacked
+    # table [L, 2^T, F] (HashEmbedder.table, marked with ``_hn_levels``).  The
+    # optimizer state dict is converted both ways so that a checkpoint written
+    # by either side (run_nerf.py:663-680) loads into the other: the stacked
+    # parameter is listed as L consecutive params whose exp_avg / exp_avg_sq are
+    # its per-level slices, with the shared step counter.
+    @staticmethod
+    def _levels(p) -> int:
+        return int(getattr(p, "_hn_levels", 0) or 0)
+
+    def state_dict(self):
+        sd = super().state_dict()
+        if not any(self._levels(p) for g in self.param_groups for p in g["params"]):
+            return sd
+        state, groups, nxt = {}, [], 0
+        for gsd, group in zip(sd["param_groups"], self.param_groups):
+            ids = []
+            for old, p in zip(gsd["params"], group["params"]):
+                st = sd["state"].get(old)
+                n = self._levels(p)
+                for l in range(max(n, 1)):
+                    if st is not None:
+                        state[nxt] = st if not n else {
+                            k: (v[l] if torch.is_tensor(v) and v.dim() == p.dim() else v)
+                            for k, v in st.items()}
+                    ids.append(nxt)
+                    nxt += 1
+            groups.append({**gsd, "params": ids})
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, state_dict):
+        """Accepts this optimizer's own state dict and the reference's (one
+        param entry per hash level in the embedding group)."""
+        sd_groups = state_dict["param_groups"]
+        if len(sd_groups) != len(self.param_groups):
+            return super().load_state_dict(state_dict)   # torch raises its own error
+        state, groups, nxt = {}, [], 0
+        src = state_dict["state"]
+        for gsd, group in zip(sd_groups, self.param_groups):
+            ids = list(gsd["params"])
+            own = len(group["params"])
+            expanded = sum(max(self._levels(p), 1) for p in group["params"])
+            if len(ids) == own:                        # this optimizer's own layout
+                new_ids = []
+                for i in ids:
+                    if i in src:
+                        state[nxt] = src[i]
+                    new_ids.append(nxt)
+                    nxt += 1
+                groups.append({**gsd, "params": new_ids})
+                continue
+            if len(ids) != expanded:
+                raise ValueError(
+                    f"loaded state dict has a group with {len(ids)} params; this optimizer's group has "
+                    f"{own} (or {expanded} with per-level hash tables)")
+            new_ids, k = [], 0
+            for p in group["params"]:
+                n = self._levels(p)
+                if not n:
+                    if ids[k] in src:
+                        state[nxt] = src[ids[k]]
+                    k += 1
+                else:
+                    parts = [src.get(i) for i in ids[k:k + n]]
+                    k += n
+                    if any(s is not None for s in parts):
+                        if any(s is None for s in parts):
+                            raise ValueError("per-level hash-table state is missing for some levels")
+                        steps = {int(s["step"]) for s in parts}
+                        if len(steps) != 1:
+                            raise ValueError(f"per-level hash-table steps differ: {sorted(steps)}")
+                        state[nxt] = {"step": steps.pop(),
+                                      "exp_avg": torch.stack([s["exp_avg"] for s in parts], 0),
+                                      "exp_avg_sq": torch.stack([s["exp_avg_sq"] for s in parts], 0)}
+                new_ids.append(nxt)
+                nxt += 1
+            groups.append({**gsd, "params": new_ids})
+        return super().load_state_dict({"state": state, "param_groups": groups})

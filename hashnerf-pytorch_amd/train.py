@@ -116,7 +116,7 @@ def default_args(**over):
              precrop_frac=0.5, finest_res=512, log2_hashmap_size=19, sparse_loss_weight=1e-10,
              tv_loss_weight=1e-6, netchunk=1024 * 64, chunk=1024 * 32, dataset_type="blender",
              i_embed=1, i_embed_views=2, no_reload=True, ft_path=None, basedir=None, expname=None,
-             H=400, W=400, n_train=100, lindisp=False, no_ndc=False, tv_until=1000)
+             H=400, W=400, n_train=100, lindisp=False, no_ndc=False, tv_until=1001)
     a.update(over)
     return types.SimpleNamespace(**a)
 
@@ -248,6 +248,12 @@ class Trainer:
         self.global_step = self.start
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(1000003 * seed + 7919 * rank + 1)
+        # draw_batch takes the stratified jitter and importance uniforms from
+        # the device's default generator (so the explicit, autograd and
+        # reference-path modes see the same numbers): after the identical
+        # init, every rank but 0 re-seeds it so DP ranks do not share them
+        if rank > 0 and self.device.type == "cuda":
+            torch.cuda.manual_seed(1000003 * seed + 7919 * rank + 2)
         self.cpu_gen = torch.Generator().manual_seed(seed * 31 + rank)
         H, W = data.H, data.W
         jj, ii = torch.meshgrid(torch.arange(H, device=self.device), torch.arange(W, device=self.device),
@@ -259,6 +265,10 @@ class Trainer:
         self.coords_crop = torch.stack([cj, ci], -1).reshape(-1, 2)
         self.crop = (H // 2 - dH, W // 2 - dW, 2 * dH, 2 * dW)
         self._grads = None
+        # the render backward's sticky fault word (hn_device_faults) is read
+        # every this many steps: one blocking copy, so a failed internal wait
+        # can never leave silently wrong gradients behind for long
+        self.fault_check_every = 100
 
     def sample_rays(self, i: int):
         """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
@@ -312,14 +322,15 @@ class Trainer:
         self._one = torch.ones((), device=self.device)
         self._grads = True
 
-    def draw_batch(self, i: int):
-        """The random inputs of step i, drawn the way run_nerf.py:576-605 and
+    def draw_batch(self, i: Optional[int] = None):
+        """The random inputs of step i (default: the next step, global_step + 1), drawn the way run_nerf.py:576-605 and
         render_rays draw them: the image (host generator), N_rand pixels
         without replacement (device sampler, centre crop before
         precrop_iters), the stratified jitter t_rand and importance uniforms u
         (device RNG), and the TV cubes + min vertices (rank 0, i <= tv_until).
         Returns a dict rays [B, 11], target [B, 3], t_rand, u, tv (or None)."""
         a, d, kw = self.args, self.data, self.kw_train
+        i = self.global_step + 1 if i is None else i
         B = a.N_rand
         img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
         crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
@@ -366,10 +377,19 @@ class Trainer:
             p.grad = g
         return lo[0], lo[1]
 
-    def step(self, i: int, batch=None):
+    def step(self, i: Optional[int] = None, batch=None):
         """One iteration; ``batch`` (explicit mode) = draw_batch(i) drawn by
-        the caller, e.g. to feed the same inputs to a reference path."""
+        the caller, e.g. to feed the same inputs to a reference path.
+
+        ``i`` is the reference loop's index (run_nerf.py:538-541: ``start + 1``
+        onwards, so 1 on a fresh run, global_step + 1 after a resume); it
+        defaults to exactly that.  The windows follow the reference: the
+        centre crop while i < precrop_iters (steps 1..499), TV while
+        i <= tv_until (1001: the weight is zeroed after the loss of step
+        i > 1000 is formed, run_nerf.py:636-638), and the lr set after the
+        step from the pre-increment global_step (:647-651)."""
         a = self.args
+        i = self.global_step + 1 if i is None else i
         if batch is not None and self.mode != "explicit":
             raise ValueError("Trainer.step(batch=...) needs mode='explicit'")
         if self.mode == "explicit":
@@ -404,4 +424,7 @@ class Trainer:
         for g in self.optimizer.param_groups:
             g["lr"] = new_lr
         self.global_step += 1
+        if self.fault_check_every and self.global_step % self.fault_check_every == 0 and \
+                self.device.type == "cuda":
+            HF.L.check_device_faults()
         return loss, mse

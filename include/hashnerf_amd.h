@@ -4,8 +4,9 @@
  * Plain pointers + sizes, no torch types.  Every pointer is a DEVICE pointer
  * (HBM, fp32, contiguous, row-major) unless documented otherwise; config
  * structs are HOST pointers read at call time.  `stream` is a hipStream_t
- * passed as void*.  The library never allocates, frees or synchronises:
- * scratch comes in through `workspace`; outputs are caller-allocated.
+ * passed as void*.  The library never allocates or frees, and synchronises
+ * only in hn_device_faults: scratch comes in through `workspace`; outputs are
+ * caller-allocated.
  * Gradient outputs named d* are ACCUMULATED (+=) so the caller zeroes them,
  * mirroring autograd's .grad accumulation.  Return value: 0 on success,
  * a positive HN_E_* code for argument errors, or a hipError_t + 1000.
@@ -23,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 3
+#define HN_ABI_VERSION 4
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -68,6 +69,15 @@ typedef struct hn_mlp_grad {
 
 int32_t hn_abi_version(void);
 const char* hn_status_string(int32_t status);
+/* Sticky device fault word.  The persistent render backward synchronises its
+ * waves through bounded LDS waits; a wait that runs out (a protocol failure,
+ * never expected) sets a bit here instead of hanging the GPU: 1 ring slot,
+ * 2 ring drain (tiles left unscattered), 4 coarse-grad flag, 8 dW buffer.
+ * Nonzero means the gradients of the launches since the last clear are
+ * invalid.  This is the one entry point that synchronises (a blocking copy
+ * from the device); call it at points where the host syncs anyway.
+ * *faults = the word; clear != 0 resets it. */
+int32_t hn_device_faults(int32_t* faults, int32_t clear);
 
 /* ---- L1 encodings --------------------------------------------------------
  * HashEmbedder.forward (hash_encoding.py:84-110): x[n][3] -> feat[n][L*F],

@@ -23,7 +23,7 @@ scene = sys.argv[2] if len(sys.argv) > 2 else "uniform"
 data = SyntheticBlender(400, 400, 100, dev, seed=0, scene=scene)
 tr = Trainer(args, data, dev)
 for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 10):
-    tr.step(i)
+    tr.step()
 rays, _ = HF.sample_rays(data.images[3], data.poses[3], 4096, data.K, 2., 6., (0, 0, 400, 400), 99)
 HF.DEBUG_KEEP = True
 with torch.no_grad():

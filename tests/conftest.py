@@ -9,6 +9,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# every render backward in the tests is followed by a read of the device fault
+# word (hn_device_faults): a failed internal wait fails the test that caused it
+os.environ.setdefault("HN_CHECK_FAULTS", "1")
 
 
 def pytest_configure(config):

@@ -54,3 +54,67 @@ def test_checkpoint_round_trip_reference_keys(hn, tmp_path):
     # ft_path takes precedence over the experiment directory
     kw3, _, start3, _, _ = create_nerf(_args(hn, tmp_path, no_reload=False, ft_path=str(ckpt)), device="cpu")
     assert start3 == 100 and torch.equal(kw3["embed_fn"].table, kw["embed_fn"].table)
+
+
+def _reference_layout_state(kw, grad_vars, T, step=7):
+    """An optimizer state dict in the reference's layout (run_nerf_helpers.py:132-135):
+    group 0 = the ten NeRFSmall weights, group 1 = the 16 per-level
+    nn.Embedding weights [2^T, 2], each with its own moments."""
+    import torch.nn as nn
+
+    from hashnerf_pytorch_amd.radam import RAdam
+    levels = [nn.Parameter(torch.zeros(2 ** T, 2)) for _ in range(16)]
+    mlp = [nn.Parameter(torch.zeros_like(p)) for p in grad_vars]
+    ref = RAdam([{"params": mlp, "weight_decay": 1e-6}, {"params": levels, "eps": 1e-15}],
+                lr=0.01, betas=(0.9, 0.99))
+    g = torch.Generator().manual_seed(5)
+    for p in mlp + levels:
+        ref.state[p] = {"step": step, "exp_avg": torch.randn(p.shape, generator=g),
+                        "exp_avg_sq": torch.rand(p.shape, generator=g)}
+    return ref.state_dict()
+
+
+def test_optimizer_state_reference_layout_loads(hn, tmp_path):
+    """a reference checkpoint's optimizer state (16 embedding
+    params) loads into the stacked-table optimizer, and this optimizer's state
+    dict is written in the reference's layout (so the reference can resume)."""
+    from hashnerf_pytorch_amd.create import create_nerf
+    torch.manual_seed(0)
+    T = 10
+    kw, _, _, grad_vars, opt = create_nerf(_args(hn, tmp_path), device="cpu")
+    sd = _reference_layout_state(kw, grad_vars, T)
+    assert [len(g["params"]) for g in sd["param_groups"]] == [10, 16]
+    opt.load_state_dict(sd)
+    table = kw["embed_fn"].table
+    st = opt.state[table]
+    assert st["step"] == 7 and st["exp_avg"].shape == table.shape
+    for l in range(16):
+        assert torch.equal(st["exp_avg"][l], sd["state"][10 + l]["exp_avg"])
+        assert torch.equal(st["exp_avg_sq"][l], sd["state"][10 + l]["exp_avg_sq"])
+    for i, p in enumerate(grad_vars):
+        assert torch.equal(opt.state[p]["exp_avg"], sd["state"][i]["exp_avg"])
+    # written back in the reference's layout, bit-identical
+    out = opt.state_dict()
+    assert [len(g["params"]) for g in out["param_groups"]] == [10, 16]
+    assert out["param_groups"][1]["eps"] == 1e-15 and out["param_groups"][0]["weight_decay"] == 1e-6
+    for i in range(26):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(out["state"][i][k], sd["state"][i][k]), (i, k)
+        assert out["state"][i]["step"] == 7
+    # and it survives torch.save / torch.load(weights_only=True)
+    path = tmp_path / "opt.tar"
+    torch.save(out, path)
+    back = torch.load(path, weights_only=True)
+    kw2, _, _, _, opt2 = create_nerf(_args(hn, tmp_path), device="cpu")
+    opt2.load_state_dict(back)
+    assert torch.equal(opt2.state[kw2["embed_fn"].table]["exp_avg"], st["exp_avg"])
+
+
+def test_optimizer_state_layout_mismatch_raises(hn, tmp_path):
+    from hashnerf_pytorch_amd.create import create_nerf
+    kw, _, _, grad_vars, opt = create_nerf(_args(hn, tmp_path), device="cpu")
+    sd = _reference_layout_state(kw, grad_vars, 10)
+    sd["param_groups"][1]["params"] = sd["param_groups"][1]["params"][:15]
+    import pytest
+    with pytest.raises(ValueError):
+        opt.load_state_dict(sd)

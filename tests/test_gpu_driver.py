@@ -133,7 +133,7 @@ def test_trainer_explicit_matches_autograd(hn):
                             sparse_loss_weight=1e-3)
         tr = Trainer(args, data, DEV, mode=mode)
         torch.manual_seed(123)
-        loss, mse = tr.step(0)
+        loss, mse = tr.step()
         res[mode] = (float(loss.detach()), float(mse), tr.embed_fn.table.grad.clone(),
                      [p.grad.clone() for p in tr.kw_train["network_fn"].weights() +
                       tr.kw_train["network_fine"].weights()])
@@ -143,3 +143,37 @@ def test_trainer_explicit_matches_autograd(hn):
     assert float((te - ta).norm() / ta.norm()) < 1e-5
     for x, y in zip(we, wa):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_trainer_step_index_follows_reference_loop(hn):
+    """Trainer.step() without an index uses the reference loop's
+    i = global_step + 1 (run_nerf.py:538-541), so TV is on through i <= tv_until
+    and the precrop window covers i < precrop_iters, also after a resume."""
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(32, 32, 2, DEV, seed=0)
+    args = default_args(N_rand=64, log2_hashmap_size=12, tv_loss_weight=1e-4, tv_until=2)
+    tr = Trainer(args, data, DEV)
+    assert tr.global_step == 0 and args.tv_until == 2
+    assert tr.draw_batch()["tv"] is not None          # i = 1
+    tr.step()                                         # i = 1
+    tr.step()                                         # i = 2 (last TV step)
+    assert tr.global_step == 2
+    assert tr.draw_batch()["tv"] is None              # i = 3 > tv_until
+    assert default_args().tv_until == 1001            # run_nerf.py:636-638: TV through i = 1001
+
+
+@pytest.mark.gpu
+def test_device_fault_word_clear_after_fused_steps(hn):
+    """The render backward's bounded waits never run out in a normal step:
+    the sticky fault word (hn_device_faults) reads 0 after a few fused steps."""
+    import ctypes as C
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(32, 32, 2, DEV, seed=0)
+    tr = Trainer(default_args(N_rand=300, log2_hashmap_size=12), data, DEV)
+    for _ in range(3):
+        tr.step()
+    w = C.c_int32(-1)
+    assert hn._lib.lib().hn_device_faults(C.byref(w), 0) == 0
+    assert w.value == 0
+    hn._lib.check_device_faults()

@@ -79,7 +79,7 @@ def _oracle_step(O, ref, i, batch, args, box, res, T, lr):
     loss.backward()
     with torch.no_grad():
         for (p, wd, eps), (m, v) in zip(params, state):
-            O.radam_step(p, p.grad, m, v, i + 1, lr, weight_decay=wd, eps=eps)
+            O.radam_step(p, p.grad, m, v, i, lr, weight_decay=wd, eps=eps)
     return float(torch.mean((ret["rgb_map"].detach() - batch["target"]) ** 2))
 
 
@@ -125,7 +125,7 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     curve = []
     t_hip = t_ref = 0.0
     lr = args.lrate
-    for i in range(iters):
+    for i in range(1, iters + 1):                  # the reference loop's index (run_nerf.py:538-541)
         batch = tr.draw_batch(i)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -136,15 +136,14 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         torch.cuda.synchronize()
         t_hip += t1 - t0
         t_ref += time.perf_counter() - t1
-        lr = args.lrate * (0.1 ** (i / (args.lrate_decay * 1000)))     # run_nerf.py:647-651
+        lr = args.lrate * (0.1 ** ((i - 1) / (args.lrate_decay * 1000)))   # run_nerf.py:647-651
         assert abs(lr - tr.optimizer.param_groups[0]["lr"]) <= 1e-12 * max(lr, 1.0)
-        if ((i + 1) % every == 0 and ((i + 1) > 0.8 * iters or (i + 1) % (5 * every) == 0)) \
-                or i + 1 == iters:
+        if (i % every == 0 and (i > 0.8 * iters or i % (5 * every) == 0)) or i == iters:
             ph, _ = _eval_hip(hn, tr, data)
             pr, _ = _eval_oracle(O, ref, data, box, res, T)
-            curve.append(dict(iter=i + 1, psnr_hip=round(ph, 4), psnr_ref=round(pr, 4),
+            curve.append(dict(iter=i, psnr_hip=round(ph, 4), psnr_ref=round(pr, 4),
                               diff=round(ph - pr, 4)))
-            print(f"iter {i + 1}: PSNR hip {ph:.3f}  ref {pr:.3f}  diff {ph - pr:+.3f}", flush=True)
+            print(f"iter {i}: PSNR hip {ph:.3f}  ref {pr:.3f}  diff {ph - pr:+.3f}", flush=True)
     # the statistic: median PSNR over the evaluations in the last 20 % of the
     # run (a single evaluation swings with the optimizer's step noise)
     tail = [c for c in curve if c["iter"] > 0.8 * iters] or curve[-1:]
@@ -160,9 +159,9 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     for sd in range(seed + 1, seed + seeds + 1):
         t2 = Trainer(args, data, DEV, seed=sd)
         ps = []
-        for i in range(iters):
+        for i in range(1, iters + 1):
             t2.step(i)
-            if (i + 1) % every == 0 and (i + 1) > 0.8 * iters:
+            if i % every == 0 and i > 0.8 * iters:
                 ps.append(_eval_hip(hn, t2, data)[0])
         spread.append(round(float(np.median(ps)), 4))
     if spread:
