@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 4                 # HN_ABI_VERSION
+ABI_VERSION = 5                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -61,7 +61,7 @@ class HnRenderBwdArgs(C.Structure):
     _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("noise_c", _P), ("noise_f", _P), ("table", _P),
                 ("coarse", HnMlp), ("fine", HnMlp), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P),
                 ("raw_f", _P), ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32),
-                ("reserved", C.c_int32), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
+                ("d_table_mode", C.c_int32), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
 
@@ -149,7 +149,7 @@ def check(status: int, what: str):
 
 
 FAULT_BITS = {1: "ring slot wait", 2: "ring drain (tiles left unscattered)", 4: "coarse-grad flag wait",
-              8: "dW buffer wait"}
+              8: "dW buffer wait", 16: "binned-scatter overflow records exhausted"}
 
 
 def check_device_faults(clear: bool = True):

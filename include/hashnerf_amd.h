@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 4
+#define HN_ABI_VERSION 5
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -72,7 +72,8 @@ const char* hn_status_string(int32_t status);
 /* Sticky device fault word.  The persistent render backward synchronises its
  * waves through bounded LDS waits; a wait that runs out (a protocol failure,
  * never expected) sets a bit here instead of hanging the GPU: 1 ring slot,
- * 2 ring drain (tiles left unscattered), 4 coarse-grad flag, 8 dW buffer.
+ * 2 ring drain (tiles left unscattered), 4 coarse-grad flag, 8 dW buffer,
+ * 16 binned-scatter overflow records exhausted (gradient records lost).
  * Nonzero means the gradients of the launches since the last clear are
  * invalid.  This is the one entry point that synchronises (a blocking copy
  * from the device); call it at points where the host syncs anyway.
@@ -178,7 +179,8 @@ typedef struct hn_render_bwd_args {
   const float* feat;        /* from the forward (saved hash features) */
   int32_t weights_packed;   /* nonzero: `workspace` is the one hn_render_fwd used and the weights
                                are unchanged since, so its packed MFMA copies are reused */
-  int32_t reserved;
+  int32_t d_table_mode;     /* 0: d_table += gradient (as every d* output); 1: d_table = gradient
+                               (every entry written, the caller need not zero it) */
   /* upstream grads (NULL = 0) */
   const float* g_rgb; const float* g_depth; const float* g_acc; const float* g_sparsity;
   const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;

@@ -19,3 +19,4 @@ for r in rows[:14]:
     print(f'{float(r["TotalDurationNs"])/1e6:8.3f} ms {r["Calls"]:>5} avg {float(r["AverageNs"])/1e3:9.2f} us {float(r["Percentage"]):5.1f}%  {r["Name"][:70]}')
 print("total GPU ms", round(tot / 1e6, 3))
 EOF
+rm -f $OUT/prof_$TAG/prof_kernel_trace.csv   # per-dispatch rows: large

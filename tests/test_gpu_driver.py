@@ -169,7 +169,7 @@ def test_device_fault_word_clear_after_fused_steps(hn):
     the sticky fault word (hn_device_faults) reads 0 after a few fused steps."""
     import ctypes as C
     from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
-    data = SyntheticBlender(32, 32, 2, DEV, seed=0)
+    data = SyntheticBlender(64, 64, 2, DEV, seed=0)    # precrop window 32x32 >= 300 rays
     tr = Trainer(default_args(N_rand=300, log2_hashmap_size=12), data, DEV)
     for _ in range(3):
         tr.step()
