@@ -78,10 +78,9 @@ struct B1K {
 
 // Backward schedules (render_bwd_kernel MODE):
 //   kModeAtomic  MLP waves 0-2 + a scatter wave issuing float atomics (fused)
-//   kModeBins    the same, the scatter wave (and MLP waves when the ring is full) writing records
 //   kModeSplit   MLP backward only (wave 0 coarse units, waves 1-3 fine units), the fine feature
 //                grads stored for scatter_bins_kernel
-enum : int { kModeAtomic = 0, kModeBins = 1, kModeSplit = 2 };
+enum : int { kModeAtomic = 0, kModeSplit = 2 };
 
 struct Ray {
   float o[3], d[3], vd[3], near, far, dnorm;
@@ -400,8 +399,7 @@ constexpr int kVoxF = 16 * 16 * 8 + kCarryF;               // scatter wave's vox
 #endif
 constexpr int kQ = HN_COMPACT ? 512 : 0;
 constexpr int kSyncInts = 5 + 2 * kSlots;
-constexpr int kBinLdsInts = 1024;                          // binned scatter: per-bin record counts
-constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + 2 * kQ + kGsLds + kSyncInts + kBinLdsInts;
+constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + 2 * kQ + kGsLds + kSyncInts;
 static_assert(kB1LdsF * 4 <= 160 * 1024, "LDS budget");
 static_assert(kB1Img >= W_END, "final dW reduction reuses the images");
 static_assert(kRRows * kXS % 4 == 0 && kXS % 4 == 0 && kSlotF % 4 == 0, "b128 alignment");
@@ -1039,7 +1037,6 @@ struct Ring {
   int* ready;   // [kSlots] ticket + 1 of the slot's contents
   int* freed;   // [kSlots] times consumed
   const float* gsl;
-  uint32_t* bcnt;   // LDS per-bin record counts (binned scatter)
 };
 
 // Sticky device fault word (hn_device_faults): a bounded wait that runs out
@@ -1111,33 +1108,33 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
   lds_fence_wave();
 }
 
-// ---- binned table-gradient scatter -----------------------------------------
+// ---- binned table-gradient scatter (HN_SCATTER=split) ----------------------
 // The memory-side float-atomic rate (~20 G requests/s, one per 64-B segment
 // of a wave-instruction) bounds the atomic scatter.  The binned scatter sends
-// no atomic to memory at all: the scatter wave writes each run head's x-pair
-// of a corner row as one 20-B record {4 sums: (x0 f0, x0 f1, x1 f0, x1 f1),
-// entry word} into the region of its bin (2^bin_shift consecutive table
-// entries, level-major: a bin is a slice of one level's rows, or whole levels
-// when T is small); bin_reduce_kernel then owns each bin, sums its records
-// with LDS atomics and writes the slice of the gradient once.  Entry word =
-// (l << T) + h(x0) | nbits << 28: the x1 corner's row is h(x0) ^ ((2^nbits -
-// 1) & mask), since the x prime is 1 and x1 = x0 + 1 differs from x0 in its
-// trailing ones and the bit above (nbits <= 11 for cells <= 1024, so both
-// rows always fall in one 2^14-entry bin).
-// Layout (floats from B1K::bins): vals f32x4 [nbins][kBwdBlocks][cap] (a
-// bin's regions are contiguous for its owner) then kOvfRecs overflow
-// records, idx u32 over the same record index, counts u32 [nbins][kBwdBlocks],
-// overflow count.  The scatter wave counts its records
-// per bin in LDS (ds_add_rtn); a region that is full spills to the shared
-// overflow records (one returning global atomic each, rare by sizing).
+// no float atomic to memory: each run head's x-pair of a corner row becomes
+// one 20-B record {4 sums: (x0 f0, x0 f1, x1 f0, x1 f1), entry word}, written
+// into the region of its bin (2^bin_shift consecutive table entries,
+// level-major); bin_reduce_kernel then owns each bin and writes its slice of
+// the gradient once.  Entry word = (l << T) + h(x0) | nbits << 28: the x1
+// corner's row is h(x0) ^ ((2^nbits - 1) & mask), since the x prime is 1 and
+// x1 = x0 + 1 differs from x0 in its trailing ones and the bit above (nbits
+// <= 11 for cells <= 1024, so both rows fall in one 2^13-entry bin).
+// Layout (floats from bins): vals f32x4 [nbins][kBwdBlocks][cap] (a bin's
+// regions are contiguous for its owner) then kOvfRecs overflow records; idx
+// u32 over the same record index; counts u32 [nbins][kBwdBlocks]; max |value|
+// bits u32 [nbins][kBwdBlocks]; overflow count.  The producer counts its
+// records per bin in LDS (ds_add_rtn) and keeps the bin's largest |value|
+// (ds_max_u32 on the float bits: the owner's fixed-point scale); a full region
+// spills to the shared overflow records (one returning global atomic each,
+// rare by sizing).
 constexpr int kOvfRecs = 1 << 20;
-constexpr int kMaxBinsLds = 1024;   // LDS counters of the scatter wave (T <= 20)
 enum : int { kFaultBins = 16 };
 
 struct BinW {
   f32x4* vals;
   uint32_t* idx;
-  uint32_t* lcnt;      // LDS [nbins]
+  uint32_t* lcnt;      // LDS [nbins] record counts
+  uint32_t* lmax;      // LDS [nbins] largest |value| bits
   uint32_t* ovf_cnt;
   size_t base;         // first record of this block's region of bin 0
   size_t stride;       // records between a block's regions of consecutive bins
@@ -1147,21 +1144,6 @@ struct BinW {
 
 __host__ __device__ inline size_t bin_records(int nbins, int cap) {
   return (size_t)kBwdBlocks * nbins * cap + kOvfRecs;
-}
-
-HN_DEV BinW bin_view(const B1K& k, uint32_t* lcnt) {
-  BinW b;
-  const size_t nrec = bin_records(k.nbins, k.bin_cap);
-  b.vals = reinterpret_cast<f32x4*>(k.bins);
-  b.idx = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
-  b.ovf_cnt = b.idx + nrec + (size_t)kBwdBlocks * k.nbins;
-  b.lcnt = lcnt;
-  b.base = (size_t)blockIdx.x * k.bin_cap;
-  b.stride = (size_t)kBwdBlocks * k.bin_cap;
-  b.ovf_base = (size_t)kBwdBlocks * k.nbins * k.bin_cap;
-  b.cap = (uint32_t)k.bin_cap;
-  b.shift = (uint32_t)k.bin_shift;
-  return b;
 }
 
 // Segmented suffix sum over runs of samples in one voxel along a 16-lane
@@ -1197,6 +1179,9 @@ HN_DEV void emit_record(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx,
   const uint32_t flat = (l << log2T) + ((cx ^ yy ^ zz) & mask);
   const uint32_t nbits = (uint32_t)__builtin_ctz(~cx) + 1u;
   const uint32_t bin = flat >> bw.shift;
+  const uint32_t mx = max(max(__float_as_uint(v[0]) & 0x7fffffffu, __float_as_uint(v[1]) & 0x7fffffffu),
+                          max(__float_as_uint(v[2]) & 0x7fffffffu, __float_as_uint(v[3]) & 0x7fffffffu));
+  __hip_atomic_fetch_max(bw.lmax + bin, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   const uint32_t slot = __hip_atomic_fetch_add(bw.lcnt + bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   size_t r = bw.base + (size_t)bin * bw.stride + slot;
   bool ok = true;
@@ -1210,31 +1195,6 @@ HN_DEV void emit_record(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx,
     bw.vals[r] = f32x4{v[0], v[1], v[2], v[3]};
     bw.idx[r] = flat | (nbits << 28);
   }
-}
-
-// One level of the binned scatter for the 16 points of a pass: lane (corner
-// row c = 2j + k, point pp) forms its row's x-pair for both features with the
-// products of scatter_level_x / trilerp_bwd (((g * wz) * wy) * wx), sums the
-// runs of samples in one voxel along the row (the same segmented suffix sum),
-// and every run head writes one record.
-HN_DEV void scatter_level_bins(const GridArgs& g, const BinW& bw, const f32x4 v0, const float2 v1, uint32_t l,
-                               float g0, float g1, int lane) {
-  const int pp = lane & 15, c = lane >> 4;
-  const uint32_t cx = (uint32_t)__float_as_int(v0.x), y0 = (uint32_t)__float_as_int(v0.y),
-                 z0 = (uint32_t)__float_as_int(v0.z);
-  const float w[3] = {v0.w, v1.x, v1.y};
-  const float wz = (c & 1) ? w[2] : 1.f - w[2];
-  const float wy = (c & 2) ? w[1] : 1.f - w[1];
-  const float a0 = (g0 * wz) * wy, a1 = (g1 * wz) * wy;
-  const float ax = 1.f - w[0];
-  float v[4] = {a0 * ax, a1 * ax, a0 * w[0], a1 * w[0]};
-  const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
-  const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
-  const uint32_t pm = (uint32_t)__ballot(head) & 0xffffu;
-  const uint32_t nz1 = ~pm & 0xfffeu, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
-  seg_sum4(v, pm, pp, nz1 != 0u, nz2 != 0u, nz4 != 0u, (nz4 & (nz4 >> 4)) != 0u);
-  if (head)
-    emit_record(bw, l, (uint32_t)g.log2T, cx, (c & 2) ? y0 + kPrimeY : y0, (c & 1) ? z0 + kPrimeZ : z0, v);
 }
 
 // ---- split backward: the table-gradient scatter as its own kernel ---------
@@ -1258,21 +1218,22 @@ struct ScK {
   int32_t bin_cap, bin_shift, nbins;
 };
 constexpr int kScWaves = 16;
-constexpr int kScMaxBins = 4096;   // LDS counters: T <= 22
+constexpr int kScMaxBins = 4096;   // LDS counters + maxima (32 KiB): T <= 21 at 2^13 entries per bin
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
-  __shared__ uint32_t bcnt[kScMaxBins];
+  __shared__ uint32_t bcnt[kScMaxBins], bmax[kScMaxBins];
   __shared__ float gsl[kGsLds];
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
+  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = bmax[i] = 0u;
   stage_grid_sizes(k.g, gsl);
   __syncthreads();
   BinW bw;
   const size_t nrec = bin_records(k.nbins, k.bin_cap);
   bw.vals = reinterpret_cast<f32x4*>(k.bins);
   bw.idx = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
-  bw.ovf_cnt = bw.idx + nrec + (size_t)kBwdBlocks * k.nbins;
+  bw.ovf_cnt = bw.idx + nrec + (size_t)2 * kBwdBlocks * k.nbins;
   bw.lcnt = bcnt;
+  bw.lmax = bmax;
   bw.base = (size_t)blockIdx.x * k.bin_cap;
   bw.stride = (size_t)kBwdBlocks * k.bin_cap;
   bw.ovf_base = (size_t)kBwdBlocks * k.nbins * k.bin_cap;
@@ -1332,6 +1293,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
       const float g0 = gf[0][l], g1 = gf[1][l];
       const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
+      // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
       const float gz[2][2] = {{g0 * az, g1 * az}, {g0 * w[2], g1 * w[2]}};   // [k][f]
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -1347,13 +1309,17 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
   __syncthreads();
   uint32_t* cnt = bw.idx + nrec + blockIdx.x;
-  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) cnt[(size_t)i * kBwdBlocks] = bcnt[i];
+  uint32_t* mxo = cnt + (size_t)kBwdBlocks * k.nbins;
+  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
+    cnt[(size_t)i * kBwdBlocks] = bcnt[i];
+    mxo[(size_t)i * kBwdBlocks] = bmax[i];
+  }
 }
 
 // The table-gradient scatter of one slot (embedding_dense_backward of
 // hash_encoding.py:106 + trilinear backward); V = 2048-float voxel buffer.
-template <int CAP, bool BINS>
-HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl, AQ& aq, const BinW& bw) {
+template <int CAP>
+HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl, AQ& aq) {
   const int lane = lane_id();
   const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
   Ray r;
@@ -1412,16 +1378,12 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
 #endif
     }
 #endif
-    float gl[16], gl1[16];   // BINS: both features (gl = f 0); else this lane's feature f
-    const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + (BINS ? 0 : 16 * f));
+    float gl[16];
+    const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + 16 * f);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const f32x4 v = src4[c];
       gl[4 * c] = v.x; gl[4 * c + 1] = v.y; gl[4 * c + 2] = v.z; gl[4 * c + 3] = v.w;
-      if constexpr (BINS) {
-        const f32x4 u = src4[4 + c];
-        gl1[4 * c] = u.x; gl1[4 * c + 1] = u.y; gl1[4 * c + 2] = u.z; gl1[4 * c + 3] = u.w;
-      }
     }
     // voxel records are read one level ahead (one wave per SIMD: nothing
     // else hides the LDS latency)
@@ -1447,17 +1409,13 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
         if (grp) cr = *reinterpret_cast<const f32x4*>(cs + 16 * (l + 1));
 #endif
       }
-      if constexpr (BINS) {
-        scatter_level_bins(k.g, bw, c0, c1, l, gl[l], gl1[l], lane);
-      } else {
 #if HN_TILE_RUNS
-        const bool cl = (cont >> l) & 1u;
-        scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq, cl && grp == 0, cl && grp == 1, cc0,
-                             cs + 16 * l);
+      const bool cl = (cont >> l) & 1u;
+      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq, cl && grp == 0, cl && grp == 1, cc0,
+                           cs + 16 * l);
 #else
-        scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
+      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
 #endif
-      }
       if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -1474,7 +1432,6 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
 #ifndef HN_MW_SELF
 #define HN_MW_SELF 0
 #endif
-template <bool BINS>
 HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_t ray, float z, int src,
                      const f32x16& dfeat) {
   const int lane = lane_id();
@@ -1485,17 +1442,14 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
   f32x4 tw[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) tw[c] = twin ? dc[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-  // MLP waves scatter a tile themselves when the ring is full: always with
-  // the binned scatter (plain stores: the scatter work then spreads over all
-  // four waves), HN_MW_SELF with the atomic one
-  if (BINS || HN_MW_SELF) {
+  if (HN_MW_SELF) {
     const int tn = lds_load(q.tick);
     if (lds_load(&q.freed[tn % kSlots]) < tn / kSlots) {   // next slot still occupied
       if (lane == 0) atomicAdd(q.selfc, 1);
       fill_slot(X, r, z, dfeat, tw);
       static_assert(!HN_MW_SELF || !HN_COMPACT, "the compacted queue belongs to the scatter wave");
       AQ none{nullptr, 0u, 0u, 0u, {}, 0ull};
-      scatter_slot<HN_SW_VMCNT, BINS>(k, X, X + kSlotF, q.gsl, none, BINS ? bin_view(k, q.bcnt) : BinW{});
+      scatter_slot<HN_SW_VMCNT>(k, X, X + kSlotF, q.gsl, none);
       return;
     }
   }
@@ -1513,8 +1467,8 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
 // is accounted for (a ticket, or scattered by its MLP wave).  tick and selfc
 // only grow and a tile is counted before it is handled, so tick + selfc ==
 // n_tiles with t >= tick means no ticket t will ever come.
-template <int CAP, bool BINS>
-HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles, const BinW& bw) {
+template <int CAP>
+HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
   AQ aq{reinterpret_cast<float2*>(V + kVoxF), 0u, 0u, 0u, {}, 0ull};
   for (int t = 0;; ++t) {
     const int s = t % kSlots;
@@ -1541,7 +1495,7 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles, const
 #endif
     if (!have) break;
     const float* S = q.slots + s * kSlotF;
-    scatter_slot<CAP, BINS>(k, S, V, q.gsl, aq, bw);
+    scatter_slot<CAP>(k, S, V, q.gsl, aq);
     ring_publish(&q.freed[s], t / kSlots + 1);
   }
   if (HN_COMPACT) aq_drain(k.d_table, aq, lane_id());
@@ -1631,7 +1585,7 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 #if HN_ABLATE == 3   // diagnostic build: MLP backward only, the fine tiles' feature grads are dropped
       if (dfeat[0] == 1234.5f && dfeat[1] == -1234.5f) X[lane] = dfeat[2] + zq[t] + (float)srcq[t];
 #else
-      ring_put<MODE == kModeBins>(k, *ring, X, r, ray, zq[t], srcq[t], dfeat);
+      ring_put(k, *ring, X, r, ray, zq[t], srcq[t], dfeat);
 #endif
       HN_LAP(pc, scat);
     } else {
@@ -1658,7 +1612,7 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0 && threadIdx.x == 0) {   // binned scatter: no overflow records yet
     const size_t nrec = bin_records(k.nbins, k.bin_cap);
-    reinterpret_cast<uint32_t*>(k.bins + 4 * nrec)[nrec + (size_t)kBwdBlocks * k.nbins] = 0u;
+    reinterpret_cast<uint32_t*>(k.bins + 4 * nrec)[nrec + (size_t)2 * kBwdBlocks * k.nbins] = 0u;
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -1759,11 +1713,7 @@ HN_DEV void dw_zero(DW& dw) {
 template <int CAP, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void render_bwd_kernel(B1K k) {
-  constexpr bool BINS = MODE == kModeBins;
   constexpr bool SPLIT = MODE == kModeSplit;
-  static_assert(!BINS || (!HN_TILE_RUNS && !HN_COMPACT),
-                "the binned scatter replaces the atomic-issue variants");
-  static_assert(kBinLdsInts >= kMaxBinsLds, "LDS bin counters");
   extern __shared__ f32x4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   const int wave = threadIdx.x >> 6;
@@ -1775,13 +1725,10 @@ void render_bwd_kernel(B1K k) {
   // [0] coarse rays done, [1] fine units taken, [2] ring tickets, [3] dW buffer zeroed,
   // [4] self-scattered tiles, [5..) ready, freed
   int* sync = reinterpret_cast<int*>(gsl + kGsLds);
-  uint32_t* bcnt = reinterpret_cast<uint32_t*>(sync + kSyncInts);
   stage_grid_sizes(k.g, gsl);
   if (threadIdx.x < kSyncInts) sync[threadIdx.x] = 0;
-  if constexpr (BINS)
-    for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
   __syncthreads();
-  const Ring ring{slots, &sync[2], &sync[4], &sync[5], &sync[5 + kSlots], gsl, bcnt};
+  const Ring ring{slots, &sync[2], &sync[4], &sync[5], &sync[5 + kSlots], gsl};
   const int64_t nb = gridDim.x;
   const int n_rays = k.B > (int64_t)blockIdx.x ? (int)((k.B - 1 - blockIdx.x) / nb + 1) : 0;
   // ray of the block's i-th unit: a contiguous chunk per block when the
@@ -1809,16 +1756,7 @@ void render_bwd_kernel(B1K k) {
   const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #endif
   if (wave == kMW && !SPLIT) {
-    BinW bw{};
-    if constexpr (BINS) bw = bin_view(k, bcnt);
-    ring_drain<CAP, BINS>(k, ring, V, HN_ABLATE == 3 ? 0 : 2 * kSf / 64 * n_rays, bw);
-    if constexpr (BINS) {
-      // this block's record count per bin (the owner reads min(count, cap)
-      // records of the region; the rest went to the overflow records)
-      lds_fence_wave();
-      uint32_t* cnt = bw.idx + bin_records(k.nbins, k.bin_cap) + blockIdx.x;
-      for (int i = lane; i < k.nbins; i += 64) cnt[(size_t)i * kBwdBlocks] = bcnt[i];
-    }
+    ring_drain<CAP>(k, ring, V, HN_ABLATE == 3 ? 0 : 2 * kSf / 64 * n_rays);
 #if HN_PROFILE
     if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
 #endif
@@ -1921,9 +1859,26 @@ __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const flo
 
 // Owner pass of the binned scatter: workgroup b sums every record of bin b
 // (the regions of all kBwdBlocks producers, then the overflow records that
-// belong to it) into its slice of 2^shift entries held in LDS (ds_add_f32),
-// and writes the slice of the table gradient once: = (overwrite) or +=.
-// Every entry of the table is written by exactly one workgroup.
+// belong to it) and writes its slice of 2^shift entries of the table
+// gradient once: = (overwrite) or +=.  Every entry is written by exactly one
+// workgroup.
+//
+// The sums are exact integer sums.  On gfx950 ds_add_f32 runs ~20x slower than
+// integer LDS atomics (config 2: ~600 us for the bins' 71 M float adds, against
+// ~145 us with ds_add_u32 on the same addresses, ~125 us for the record loads
+// alone), and a bin's records are heavily duplicated (surfaces: e.g. 37.5 K
+// records on 2.9 K distinct entries at level 8), which defeats claiming
+// entries for plain read-modify-writes.  So each value is converted to a
+// 64-bit fixed-point integer in units of 2^(E - 40), E the exponent of the
+// bin's largest |value| (every value < 2^41 units, 2^20 of them < 2^61), and
+// added with ds_add_u64; the slice is converted back (one rounding to fp32).
+// Integer adds are associative, so the gradient is bitwise reproducible, and
+// every entry keeps full fp32 precision down to 2^-16 of the bin's largest
+// contribution (2^-40 absolute resolution below that).  Measured on recorded
+// config 2 bins (scripts/bin_stats.py): median relative error 1e-8 (fp32
+// sequential sums 6e-9 .. 2e-8); the worst entries, at |g| ~ 1e-17 with a bin
+// maximum ~ 5e-7, within 8e-3 -- where fp32 atomics cannot resolve them
+// either once a larger contribution has been added.
 struct BinR {
   const float* bins;
   int32_t nbins, cap, shift, log2T;
@@ -1931,113 +1886,58 @@ struct BinR {
   int32_t overwrite;
 };
 constexpr int kBinThreads = 1024;
-#ifndef HN_BR_DIAG
-#define HN_BR_DIAG 0
-#endif
 
-// LDS float add.  ds_add_f32 measured ~20x slower than ds_add_u32 on the same
-// addresses (bin_reduce on config 2: ~600 us vs ~143 us with integer adds,
-// ~126 us for the record loads alone); HN_BR_CAS=1 adds through a
-// compare-and-swap loop on the integer image instead (same sum, any order).
-#ifndef HN_BR_CAS
-#define HN_BR_CAS 0
-#endif
-HN_DEV void lds_fadd(float* p, float v) {
-#if HN_BR_CAS == 2   // diagnostic: the returning float add
-  const float o = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (o == 1234.5f) p[1] = 0.f;
-#elif HN_BR_CAS
-  uint32_t* q = reinterpret_cast<uint32_t*>(p);
-  uint32_t old = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (;;) {
-    const uint32_t want = __float_as_uint(__uint_as_float(old) + v);
-    const uint32_t seen = atomicCAS(q, old, want);
-    if (seen == old) break;
-    old = seen;
-  }
-#else
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
+HN_DEV uint32_t wave_max_u32(uint32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, shfl_from(v, lane ^ d));
+  return v;
 }
 
-HN_DEV void bin_add(float* acc, const f32x4 v, uint32_t w, uint32_t sel, uint32_t tmask) {
-#if HN_BR_DIAG == 5   // diagnostic: conflict-free addresses
-  const uint32_t e0 = (threadIdx.x * 2u) & sel, e1 = e0 + 1u;
-#else
+HN_DEV long long fx_of(float v, double scale) { return __double2ll_rn((double)v * scale); }
+
+HN_DEV void bin_add(unsigned long long* acc, const f32x4 v, uint32_t w, uint32_t sel, uint32_t tmask,
+                    double scale) {
   const uint32_t e0 = w & 0x0fffffffu & sel;
   const uint32_t e1 = e0 ^ (((1u << (w >> 28)) - 1u) & tmask);
-#endif
-#if HN_BR_DIAG == 3   // diagnostic: integer LDS atomics (wrong sums)
-  uint32_t* ai = reinterpret_cast<uint32_t*>(acc);
-  __hip_atomic_fetch_add(ai + 2 * e0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_add(ai + 2 * e0 + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_add(ai + 2 * e1, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_add(ai + 2 * e1 + 1, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return;
-#elif HN_BR_DIAG == 4   // diagnostic: plain LDS stores (wrong sums)
-  acc[2 * e0] = v.x; acc[2 * e0 + 1] = v.y; acc[2 * e1] = v.z; acc[2 * e1 + 1] = v.w;
-  return;
-#endif
-  lds_fadd(acc + 2 * e0, v.x);
-  lds_fadd(acc + 2 * e0 + 1, v.y);
-  lds_fadd(acc + 2 * e1, v.z);
-  lds_fadd(acc + 2 * e1 + 1, v.w);
+  const long long q[4] = {fx_of(v.x, scale), fx_of(v.y, scale), fx_of(v.z, scale), fx_of(v.w, scale)};
+  __hip_atomic_fetch_add(acc + 2 * e0, (unsigned long long)q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + 2 * e0 + 1, (unsigned long long)q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + 2 * e1, (unsigned long long)q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + 2 * e1 + 1, (unsigned long long)q[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Records of the bin, flattened over the producers' regions: record r is
-// found by binary search over the LDS prefix of the regions' counts.
-//
-// Accumulation (HN_BR_ROUTE=1, default).  ds_add_f32 runs ~20x slower than
-// integer LDS atomics on gfx950 (see lds_fadd), so the owner sums with plain
-// LDS read-modify-writes on entries each wave owns exclusively: per chunk of
-// 1024 records (one per thread, loaded two chunks ahead) the 2048 half-records
-// (entry, 2 floats) are routed to their owner wave ((entry >> 5) & 15) through
-// an LDS stage -- counts per (wave, owner) from ballots, one ds_add_rtn per
-// owner and wave, a 16-entry prefix -- and each owner wave applies its items
-// 64 at a time; two lanes of one instruction on the same entry are separated
-// by claiming a hashed tag byte (the lane whose id stays in it updates, the
-// others retry).  HN_BR_ROUTE=0: every record straight into LDS with
-// lds_fadd.  Overflow records (never expected) always take lds_fadd.
-#ifndef HN_BR_ROUTE
-#define HN_BR_ROUTE 1
-#endif
-#ifndef HN_BR_PROF
-#define HN_BR_PROF 0
-#endif
-#if HN_BR_PROF
-__device__ unsigned long long g_brprof[8];   // cycles of wave 0: top/count, B1, prefix+B2, stage+B3, apply; rounds, batches
-#define HN_BRT(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&g_brprof[i], n_ - t_); t_ = n_; } while (0)
-#else
-#define HN_BRT(i) ((void)0)
-#endif
-constexpr int kRtOwners = kBinThreads / 64;
-constexpr int kRtTags = 256;
-struct RtItem {
-  uint32_t e;
-  float g0, g1;
-};
-
+// Records of the bin, flattened over the producers' regions: thread i takes
+// records i, i + 1024, ... (4 at a time, independent loads in flight) and
+// finds each one's region by binary search over the LDS prefix of the
+// regions' counts.
 __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   extern __shared__ f32x4 acc4[];
   __shared__ uint32_t pre[kBwdBlocks + 1];
-  __shared__ uint32_t wsum[kBwdBlocks / 64];
-  float* acc = reinterpret_cast<float*>(acc4);
-  const int n4 = (2 << k.shift) / 4;
+  __shared__ uint32_t wsum[kBwdBlocks / 64], wmax[kBwdBlocks / 64];
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(acc4);
+  const int n4 = (2 << k.shift) / 2;   // f32x4 = 2 accumulators
   for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t b = blockIdx.x;
   const size_t nrec = bin_records(k.nbins, k.cap);
   const f32x4* vals = reinterpret_cast<const f32x4*>(k.bins);
   const uint32_t* idx = reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec);
   const uint32_t* cnt = idx + nrec;
-  const uint32_t n_ovf = cnt[(size_t)kBwdBlocks * k.nbins];
+  const uint32_t* mxs = cnt + (size_t)kBwdBlocks * k.nbins;
+  const uint32_t n_ovf = mxs[(size_t)kBwdBlocks * k.nbins];
   static_assert(kBwdBlocks == 256 && kBinThreads >= 256, "one count per thread of waves 0-3");
-  uint32_t n = 0;
+  uint32_t n = 0, mx = 0;
   if (threadIdx.x < kBwdBlocks) {
     const uint32_t c = cnt[(size_t)b * kBwdBlocks + threadIdx.x];
     n = c < (uint32_t)k.cap ? c : (uint32_t)k.cap;
+    mx = mxs[(size_t)b * kBwdBlocks + threadIdx.x];
   }
   const uint32_t inc = (uint32_t)wave_incl_sum((double)n);   // exact: counts < 2^53
-  if (threadIdx.x < kBwdBlocks && (threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+  const uint32_t wmx = wave_max_u32(mx);
+  if (threadIdx.x < kBwdBlocks && (threadIdx.x & 63) == 63) {
+    wsum[threadIdx.x >> 6] = inc;
+    wmax[threadIdx.x >> 6] = wmx;
+  }
   __syncthreads();
   if (threadIdx.x < kBwdBlocks) {
     uint32_t add = 0;
@@ -2045,154 +1945,62 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     pre[threadIdx.x + 1] = inc + add;
   }
   if (threadIdx.x == 0) pre[0] = 0;
+  // bin scale: largest |value| < 2^(E+1) -> 2^40 units; overflow records may be
+  // larger (their producers' maxima are not kept): they are clamped by the
+  // same bound below, and they never occur at the sized capacities
+  const uint32_t bmx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+  const int E = (int)((bmx >> 23) & 0xffu) - 127;
+  const double scale = ldexp(1.0, 40 - (E < -126 ? -126 : E));
   __syncthreads();
   const uint32_t total = pre[kBwdBlocks];
   const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u;
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
-  auto load = [&](uint32_t r, f32x4& v, uint32_t& w) {
-    int lo = 0;   // largest p with pre[p] <= r
-#pragma unroll
-    for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
-      if (pre[lo + st] <= r) lo += st;
-    const size_t rec = bbase + (size_t)lo * k.cap + (r - pre[lo]);
-#if HN_BR_DIAG == 2   // diagnostic: stand-in records, no record loads
-    v = f32x4{1.f, 1.f, 1.f, 1.f};
-    w = (uint32_t)(rec * 2654435761u) >> 4;
-#else
-    v = vals[rec];
-    w = idx[rec];
-#endif
-  };
-#if HN_BR_ROUTE
-  __shared__ uint32_t ocnt[kRtOwners];
-  __shared__ uint32_t obase[kRtOwners + 1];
-  __shared__ uint8_t tags[kRtOwners][kRtTags];
-  __shared__ RtItem stage[2 * kBinThreads];
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  if (threadIdx.x < kRtOwners) ocnt[threadIdx.x] = 0u;
-  f32x4 v0{}, v1{};
-  uint32_t w0 = 0u, w1 = 0u;
-  if (threadIdx.x < total) load(threadIdx.x, v0, w0);
-  if (kBinThreads + threadIdx.x < total) load(kBinThreads + threadIdx.x, v1, w1);
-  __syncthreads();   // ocnt zeroed, acc zeroed
-  float2* acc2 = reinterpret_cast<float2*>(acc);
-#if HN_BR_PROF
-  uint64_t t_ = __builtin_amdgcn_s_memtime();
-#endif
-  for (uint32_t base = 0; base < total; base += kBinThreads) {
-    const bool have = base + threadIdx.x < total;
-    const uint32_t e0 = w0 & 0x0fffffffu & sel;
-    const uint32_t e1 = e0 ^ (((1u << (w0 >> 28)) - 1u) & tmask);
-    const RtItem ia{e0, v0.x, v0.y}, ib{e1, v0.z, v0.w};
-    // records two chunks ahead
-    v0 = v1;
-    w0 = w1;
-    if (base + 2 * kBinThreads + threadIdx.x < total) load(base + 2 * kBinThreads + threadIdx.x, v1, w1);
-#if HN_BR_DIAG == 7   // diagnostic: record loads and barriers only
-    if (ia.g0 == 1234.5f && ib.e == 7u) acc[threadIdx.x] = ia.g1;
-    __syncthreads();
-    __syncthreads();
-    __syncthreads();
-    continue;
-#endif
-    // owner = entry bits 5..8: a wave's entries span every LDS bank (entry e
-    // sits in banks 2e, 2e + 1 mod 64)
-    const int oa = (int)((e0 >> 5) & (kRtOwners - 1)), ob = (int)((e1 >> 5) & (kRtOwners - 1));
-    uint32_t ra = 0u, rb = 0u, myc = 0u;
-#pragma unroll
-    for (int o = 0; o < kRtOwners; ++o) {
-      const uint64_t ma = __ballot(have && oa == o), mb = __ballot(have && ob == o);
-      const uint32_t ca = (uint32_t)__popcll(ma);
-      const uint32_t lo_a = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
-      const uint32_t lo_b = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
-      if (oa == o) ra = lo_a;
-      if (ob == o) rb = ca + lo_b;
-      if (lane == o) myc = ca + (uint32_t)__popcll(mb);
-    }
-    uint32_t wb = 0u;
-    if (lane < kRtOwners && myc) wb = __hip_atomic_fetch_add(&ocnt[lane], myc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    HN_BRT(0);
-    __syncthreads();   // (1) every wave's counts are in
-    HN_BRT(1);
-    if (wave == 0) {
-      const uint32_t c = lane < kRtOwners ? ocnt[lane] : 0u;
-      const uint32_t incl = (uint32_t)wave_incl_sum((double)c);
-      if (lane < kRtOwners) {
-        obase[lane + 1] = incl;
-        ocnt[lane] = 0u;
-      }
-      if (lane == 0) obase[0] = 0u;
-    }
-    __syncthreads();   // (2) owner segments known
-    HN_BRT(2);
-    // the owners' wave bases live in lanes 0..15: read them with every lane active
-    const uint32_t pa = obase[oa] + shfl_from(wb, oa) + ra, pb = obase[ob] + shfl_from(wb, ob) + rb;
-    if (have) {
-      stage[pa] = ia;
-      stage[pb] = ib;
-    }
-    __syncthreads();   // (3) stage written
-    HN_BRT(3);
-    const uint32_t s0 = obase[wave], s1 = HN_BR_DIAG == 6 ? s0 : obase[wave + 1];
-    for (uint32_t s = s0; s < s1; s += 64) {
-      bool pend = s + lane < s1;
-      const RtItem it = pend ? stage[s + lane] : RtItem{0u, 0.f, 0.f};
-      const uint32_t slot = (it.e * 0x9E3779B1u) >> 24;
-#if HN_BR_PROF
-      if (threadIdx.x == 0) atomicAdd(&g_brprof[6], 1ull);
-#endif
-      while (__ballot(pend)) {
-#if HN_BR_PROF
-        if (threadIdx.x == 0) atomicAdd(&g_brprof[5], 1ull);
-#endif
-        // relaxed atomics on the LDS array itself (a volatile generic pointer
-        // becomes FLAT, which waits for the record loads in flight)
-        if (pend) __hip_atomic_store(&tags[wave][slot], (uint8_t)lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (pend && __hip_atomic_load(&tags[wave][slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-                        (uint8_t)lane) {   // one claimant per tag: distinct entries
-          float2 a = acc2[it.e];
-          a.x = a.x + it.g0;
-          a.y = a.y + it.g1;
-          acc2[it.e] = a;
-          pend = false;
-        }
-#if HN_BR_DIAG == 8   // diagnostic: one claim round (losers dropped)
-        pend = false;
-#endif
-      }
-    }
-    HN_BRT(4);
-  }
-#else
   for (uint32_t r0 = threadIdx.x; r0 < total; r0 += 4 * kBinThreads) {
     f32x4 v[4];
     uint32_t w[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (r0 + q * kBinThreads < total) load(r0 + q * kBinThreads, v[q], w[q]);
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t r = r0 + q * kBinThreads;
+      if (r < total) {
+        int lo = 0;   // largest p with pre[p] <= r
+#pragma unroll
+        for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
+          if (pre[lo + st] <= r) lo += st;
+        const size_t rec = bbase + (size_t)lo * k.cap + (r - pre[lo]);
+        v[q] = vals[rec];
+        w[q] = idx[rec];
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (r0 + q * kBinThreads < total) {
-#if HN_BR_DIAG == 1   // diagnostic: record loads only, no LDS adds
-        if (v[q].x == 1234.5f && w[q] == 77u) acc[threadIdx.x] = v[q].y;
-#else
-        bin_add(acc, v[q], w[q], sel, tmask);
-#endif
-      }
+      if (r0 + q * kBinThreads < total) bin_add(acc, v[q], w[q], sel, tmask, scale);
   }
-#endif
-  __syncthreads();
   const uint32_t no = n_ovf < (uint32_t)kOvfRecs ? n_ovf : (uint32_t)kOvfRecs;
   const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
   for (uint32_t s = threadIdx.x; s < no; s += kBinThreads) {
     const uint32_t w = idx[ob + s];
-    if (((w & 0x0fffffffu) >> k.shift) == b) bin_add(acc, vals[ob + s], w, sel, tmask);
+    if (((w & 0x0fffffffu) >> k.shift) == b) {
+      f32x4 v = vals[ob + s];
+      const float lim = (float)ldexp(1.0, E + 1);   // keep within the fixed-point range
+      v.x = fminf(fmaxf(v.x, -lim), lim); v.y = fminf(fmaxf(v.y, -lim), lim);
+      v.z = fminf(fmaxf(v.z, -lim), lim); v.w = fminf(fmaxf(v.w, -lim), lim);
+      bin_add(acc, v, w, sel, tmask, scale);
+    }
   }
   __syncthreads();
-  f32x4* dst = reinterpret_cast<f32x4*>(k.d_table + ((size_t)b << (k.shift + 1)));
-  for (int i = threadIdx.x; i < n4; i += kBinThreads) {
-    f32x4 a = acc4[i];
-    if (!k.overwrite) a = a + dst[i];
+  const double inv = 1.0 / scale;
+  float4* dst = reinterpret_cast<float4*>(k.d_table + ((size_t)b << (k.shift + 1)));
+  const int nd4 = (2 << k.shift) / 4;
+  for (int i = threadIdx.x; i < nd4; i += kBinThreads) {
+    float4 a;
+    a.x = (float)((double)(long long)acc[4 * i] * inv);
+    a.y = (float)((double)(long long)acc[4 * i + 1] * inv);
+    a.z = (float)((double)(long long)acc[4 * i + 2] * inv);
+    a.w = (float)((double)(long long)acc[4 * i + 3] * inv);
+    if (!k.overwrite) {
+      const float4 d = dst[i];
+      a.x = a.x + d.x; a.y = a.y + d.y; a.z = a.z + d.z; a.w = a.w + d.w;
+    }
     dst[i] = a;
   }
 }
@@ -2211,46 +2019,42 @@ static bool grad_ok(const hn_mlp_grad& w) {
   return w.sigma0 && w.sigma1 && w.color0 && w.color1 && w.color2;
 }
 
-// Binned scatter geometry.  A bin is 2^14 consecutive table entries (128 KiB
-// of f32 pairs: the owner's LDS), or the whole table when that is smaller.
-// Region capacity per (block, bin): the records a block's rays can write
-// into one bin without any run merging on average (192 unique points x 4
-// corner rows per level and ray, spread over the level's 2^T / 2^shift
-// bins) + 128; sized so, a region overflows only on strongly clumped input.
-// HN_SCATTER=atomic selects the atomic scatter instead; T > 20 always uses it
-// (more bins than the scatter wave's LDS counters).
+// Binned scatter geometry.  A bin is 2^13 consecutive table entries (its
+// 2 x 2^13 64-bit accumulators are the owner's 128 KiB of LDS), or the whole
+// table when that is smaller.  Region capacity per (block, bin): the records
+// a block's rays can write into one bin without any run merging on average
+// (192 unique points x 4 corner rows per level and ray, spread over the
+// level's 2^T / 2^shift bins) + 128; sized so, a region overflows only on
+// strongly clumped input (into the shared overflow records).
 struct BinGeom {
   int shift, nbins, cap;
   size_t floats;
 };
 static BinGeom bin_geom(int T, int64_t n_rays) {
   BinGeom g;
-  g.shift = T + 4 < 14 ? T + 4 : 14;
+  g.shift = T + 4 < 13 ? T + 4 : 13;
   g.nbins = 1 << (T + 4 - g.shift);
   const double rpb = (double)((n_rays + kBwdBlocks - 1) / kBwdBlocks);
   const double avg = rpb * (kSf * 4) * ldexp(1.0, g.shift - T);
   g.cap = (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
   const size_t nrec = bin_records(g.nbins, g.cap);
-  g.floats = nrec * 5 + (size_t)kBwdBlocks * g.nbins + 4;
+  g.floats = nrec * 5 + (size_t)2 * kBwdBlocks * g.nbins + 4;
   return g;
 }
-// Backward schedule: HN_SCATTER = atomic (default) | split | fused.  The
-// fused binned scatter counts records in the render kernel's spare LDS
-// (nbins <= kMaxBinsLds: T <= 20), the split one in its own kernel (T <= 22).
+// Backward schedule: HN_SCATTER = atomic (default) | split.  The split
+// scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 21).
 static int bwd_mode(const hn_render_cfg* c) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("HN_SCATTER");
-    env = (e && !strcmp(e, "split")) ? kModeSplit : (e && !strcmp(e, "fused")) ? kModeBins : kModeAtomic;
+    env = (e && !strcmp(e, "split")) ? kModeSplit : kModeAtomic;
   }
-  const int nb_log2 = c ? c->grid.log2_hashmap_size + 4 - 14 : 99;
-  if (env == kModeBins && nb_log2 <= 10) return kModeBins;
-  if (env == kModeSplit && nb_log2 <= 12) return kModeSplit;
+  if (env == kModeSplit && c && (16ll << c->grid.log2_hashmap_size) <= (long long)kScMaxBins << 13) return kModeSplit;
   return kModeAtomic;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
 // coarse-pass feature grads [n][64][32] | d raw [n][256][4] | split: fine
-// feature grads [n][6][1024] | binned: records (bin_geom).
+// feature grads [n][6][1024] and the records (bin_geom).
 struct WsLayout {
   size_t dfeat_f, bins, total;
 };
@@ -2259,7 +2063,7 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32 + n * (kSc + kSf) * 4;
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
-  w.total = w.bins + (mode != kModeAtomic ? bin_geom(cfg->grid.log2_hashmap_size, n_rays).floats : 0);
+  w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays).floats : 0);
   return w;
 }
 
@@ -2400,9 +2204,6 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (mode == kModeSplit)
     hipLaunchKernelGGL((render_bwd_kernel<HN_SW_VMCNT, kModeSplit>), dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s,
                        k);
-  else if (mode == kModeBins)
-    hipLaunchKernelGGL((render_bwd_kernel<HN_SW_VMCNT, kModeBins>), dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s,
-                       k);
   else if (T >= 21)
     hipLaunchKernelGGL((render_bwd_kernel<HN_SW_VMCNT_BIG, kModeAtomic>), dim3(kBwdBlocks), dim3(64 * kB1Waves),
                        lds, s, k);
@@ -2436,7 +2237,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.d_table = a->d_table;
     r.overwrite = a->d_table_mode == 1;
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
-                       (size_t)(2 << bg.shift) * sizeof(float), s, r);
+                       (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
     if ((st = hip_status(hipGetLastError()))) return st;
 #if HN_BR_PROF
     {

@@ -56,6 +56,8 @@ def main():
     n, T = a.n_rand, a.log2T
     shift, nbins, cap = bin_geom(T, n)
     off = 2 * G_END + BLOCKS * 2 * W_END + n * 64 * 32 + n * 256 * 4
+    if os.environ.get("HN_SCATTER") == "split":
+        off += n * 192 * 32
     nrec = BLOCKS * nbins * cap + OVF
     ws = st.wsb.view(torch.int32)
     idx0 = off + 4 * nrec
@@ -70,6 +72,74 @@ def main():
         print("records per level:", " ".join(str(int(x)) for x in lv))
         mx = cnt.max(1).reshape(-1, bins_per_level).max(1)
         print("max region fill per level:", " ".join(str(int(x)) for x in mx))
+    # owner-pass simulation on a few bins: chunks of 1024 flattened records ->
+    # 2048 items (entry, owner (e >> 5) & 15); per owner batches of 64 items;
+    # the claim rounds a batch needs = max items per tag slot (hashed entry)
+    vals_i = off
+    idx_i = off + 4 * nrec
+    wsi = ws
+    sel, tmask = (1 << shift) - 1, (1 << T) - 1
+    for b in (0, nbins // 2, nbins - 1, nbins - 2):
+        c = np.minimum(cnt[b], cap)
+        recs = []
+        for p in range(BLOCKS):
+            s0 = idx_i + (b * BLOCKS + p) * cap
+            recs.append(wsi[s0:s0 + int(c[p])].cpu().numpy().view(np.uint32))
+        w = np.concatenate(recs)
+        e0 = (w & 0x0fffffff) & sel
+        d = ((np.uint32(1) << (w >> 28)) - 1) & tmask
+        e1 = e0 ^ d
+        rounds, batches, maxmult = 0, 0, 0
+        for ch in range(0, len(w), 1024):
+            ea, eb = e0[ch:ch + 1024], e1[ch:ch + 1024]
+            items = np.concatenate([np.stack([ea, eb], 1).reshape(-1)])
+            own = (items >> 5) & 15
+            for o in range(16):
+                it = items[own == o]
+                for q in range(0, len(it), 64):
+                    bt = it[q:q + 64]
+                    slot = ((bt.astype(np.uint64) * 0x9E3779B1) & 0xffffffff) >> 24
+                    m = np.bincount(slot.astype(np.int64)).max()
+                    rounds += m
+                    batches += 1
+                    maxmult = max(maxmult, np.bincount(bt.astype(np.int64)).max())
+        print(f"bin {b}: records {len(w)} distinct entries {len(np.unique(np.concatenate([e0, e1])))} "
+              f"batches {batches} rounds {rounds} ({rounds / max(batches, 1):.1f}/batch) max same-entry per batch {maxmult}")
+    # fixed-point accumulation study: per bin, scale from the max |record
+    # value| (exponent E): int64 units of 2^(E - 42); error of the rounded
+    # fixed-point sums vs exact (float64) sums, and vs fp32 sequential sums
+    vals_all = ws.view(torch.float32)
+    for b in (0, nbins // 4, nbins // 2, nbins - 1):
+        c = np.minimum(cnt[b], cap)
+        wl, vl = [], []
+        for p in range(BLOCKS):
+            r0 = (b * BLOCKS + p) * cap
+            wl.append(wsi[idx_i + r0: idx_i + r0 + int(c[p])].cpu().numpy().view(np.uint32))
+            vl.append(vals_all[vals_i + 4 * r0: vals_i + 4 * (r0 + int(c[p]))].cpu().numpy().reshape(-1, 4))
+        w, v = np.concatenate(wl), np.concatenate(vl)
+        if len(w) == 0:
+            continue
+        e0 = (w & 0x0fffffff) & sel
+        e1 = e0 ^ (((np.uint32(1) << (w >> 28)) - 1) & tmask)
+        ent = np.concatenate([2 * e0, 2 * e0 + 1, 2 * e1, 2 * e1 + 1]).astype(np.int64)
+        x = np.concatenate([v[:, 0], v[:, 1], v[:, 2], v[:, 3]])
+        exact = np.zeros(2 << shift)
+        np.add.at(exact, ent, x.astype(np.float64))
+        f32 = np.zeros(2 << shift, np.float32)
+        np.add.at(f32, ent, x)
+        E = int(np.floor(np.log2(np.abs(x).max())))
+        q = np.rint(x.astype(np.float64) * 2.0 ** (42 - E)).astype(np.int64)
+        acc = np.zeros(2 << shift, np.int64)
+        np.add.at(acc, ent, q)
+        fx = (acc.astype(np.float64) * 2.0 ** (E - 42)).astype(np.float32)
+        nz = exact != 0
+        rel = lambda a: np.abs(a[nz] - exact[nz]) / np.abs(exact[nz])
+        rf, rq = rel(f32), rel(fx)
+        print(f"bin {b}: maxexp {E} nonzero {nz.sum()} |g| min {np.abs(exact[nz]).min():.2e} median "
+              f"{np.median(np.abs(exact[nz])):.2e} | rel err fp32 median {np.median(rf):.1e} p99.9 "
+              f"{np.quantile(rf, .999):.1e} max {rf.max():.1e} | fixed64 median {np.median(rq):.1e} p99.9 "
+              f"{np.quantile(rq, .999):.1e} max {rq.max():.1e}; entries with fixed64 err > fp32 max: "
+              f"{(rq > rf.max()).sum()}")
     HF.L.check_device_faults()
     print("no device faults")
 

@@ -32,7 +32,9 @@ HN_PSNR_NTRAIN=100 HN_PSNR_OUT=path gives one paired run at 5k iterations
 is the mean over paired seeds, checked against +-0.1 dB by
 scripts/psnr_aggregate.py (scripts/gpu_psnr.sh; profiles/r01/psnr_5k.json):
 one paired run alone is checked against 0.25 dB, since equally good runs at
-different seeds land ~0.15 dB apart.
+different seeds land ~0.15 dB apart.  The short default run is a training
+smoke check: mid-climb, paired runs differ by up to ~0.6 dB either way, so it
+is held to TOL_DB_SHORT.
 """
 import json
 import math
@@ -46,8 +48,10 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 TOL_DB = 0.1          # at 5k iterations: the metric's bar, on the mean over paired seeds
-TOL_DB_RUN = 0.25     # one paired run: two equally good runs land ~0.15 dB apart at 5k iterations,
-                      # and short runs still climb ~1 dB / 100 it with 0.4 dB swings mid-run
+TOL_DB_RUN = 0.25     # one paired run at 5k iterations: two equally good runs land ~0.15 dB apart
+TOL_DB_SHORT = 0.75   # the default 400-iteration run, still climbing ~1 dB / 100 it: over seeds 0-2
+                      # the paired difference measured +0.07 / +0.15 / -0.49 dB (atomic scatter) and
+                      # +0.24 / +0.28 / -0.59 dB (binned scatter) (scripts/psnr_short_ab.sh)
 
 
 def _oracle_trainer(O, tr, dev):
@@ -166,7 +170,7 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         spread.append(round(float(np.median(ps)), 4))
     if spread:
         stat["hip_other_seeds"] = spread
-    tol = TOL_DB_RUN
+    tol = TOL_DB_RUN if iters >= 5000 else TOL_DB_SHORT
     out = dict(iters=iters, seed=seed, H=H, W=W, N_rand=args.N_rand, n_train=n_train, n_test=4,
                scene="procedural chair (train.procedural_field)", tol_db=tol, final=stat, curve=curve,
                ms_per_iter_hip=round(1e3 * t_hip / iters, 3),
