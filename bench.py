@@ -49,24 +49,28 @@ UNIQUE_PTS = 192               # per ray (the 64 coarse points recur in the fine
 PATH_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2 + 36
 BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2        # bwd kernel: re-gather + scatter-add
 FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
-BWD_KERNELS = ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel")   # hn_render_bwd
+# the kernels of one hn_render_bwd launch, per table-gradient scatter
+BWD_KERNELS = {"atomic": ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel"),
+               "binned": ("render_comp_bwd_kernel", "render_bwd_kernel", "scatter_bins_kernel",
+                          "bin_reduce_kernel", "slab_reduce_kernel")}
 
 
-def measured_traffic(cfg_id, n_rand_override, scene, pretrain):
+def measured_traffic(cfg_id, n_rand_override, scene, pretrain, scatter):
     """HBM-side bytes per hn_render_bwd launch from the last PMC passes of the
-    same workload (scripts/gpu_pmc.sh -> profiles/traffic_config<N>_<scene>_p<pretrain>.json):
+    same workload (scripts/gpu_pmc.sh -> profiles/traffic_config<N>_<scene>_p<pretrain>_<scatter>.json):
     2 x FETCH_SIZE + WRITE_SIZE summed over the launch's kernels.  PMC
     counters need their own rocprofv3 passes, so bench.py cannot collect
     them live; None when no file matches this workload."""
-    path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}_{scene}_p{pretrain}.json")
+    path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}_{scene}_p{pretrain}_{scatter}.json")
     if n_rand_override or not os.path.exists(path):
         return None, None, None
     t = json.load(open(path))
     ks = t.get("kernels", {})
-    if not all(k in ks for k in BWD_KERNELS):
+    kern = BWD_KERNELS[scatter]
+    if not all(k in ks for k in kern):
         return None, None, None
-    return (sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in BWD_KERNELS), t.get("source"),
-            sum(ks[k].get("atomic_requests", 0.0) for k in BWD_KERNELS) or None)
+    return (sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in kern), t.get("source"),
+            sum(ks[k].get("atomic_requests", 0.0) for k in kern) or None)
 
 
 def cpu_baseline(cfg, seconds=12.0, n_rays=256):
@@ -207,7 +211,8 @@ def main():
     B = cfg["N_rand"]
     value = world * B * args.steps / dt
     if rank == 0:
-        traffic, traffic_src, atomics = measured_traffic(cfg_id, args.n_rand, args.scene, args.pretrain)
+        scatter = "binned" if HF.L.lib().hn_render_scatter_mode(tr._cfg) == 2 else "atomic"
+        traffic, traffic_src, atomics = measured_traffic(cfg_id, args.n_rand, args.scene, args.pretrain, scatter)
         bwd_gbs = B * BWD_BYTES_PER_RAY / (bwd_ms * 1e-3) / 1e9
         fwd_gbs = B * FWD_BYTES_PER_RAY / (fwd_ms * 1e-3) / 1e9
         line = {
@@ -226,22 +231,15 @@ def main():
             "config": {"workload": cfg["workload"], "rays_per_gpu": B, "global_batch": B * world,
                        "samples_per_ray": "64+128", "log2_hashmap_size": cfg["log2_hashmap_size"],
                        "finest_res": cfg["finest_res"], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": "render_bwd (hn_render_bwd launch)",
+            "roofline": {"bound": "hbm",
+                         "kernel": "render_bwd (hn_render_bwd launch: " + " + ".join(BWD_KERNELS[scatter]) + ")",
                          "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic) if traffic else None,
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": B * BWD_BYTES_PER_RAY,
                          "bytes_per_ray": BWD_BYTES_PER_RAY, "launch_ms": round(bwd_ms, 4),
-                         # the binding resource of this launch: memory-side float-atomic
-                         # requests (TCC_EA0_ATOMIC, same PMC passes) per second
-                         "atomic_requests": round(atomics) if atomics else None,
-                         "atomic_Greq_per_s": round(atomics / (bwd_ms * 1e-3) / 1e9, 2) if atomics else None,
-                         # MI355X_MICROARCH.md 'Global float atomics': ~1.3 TB/s of added
-                         # bytes = 64-B memory-side requests at ~20.3 G/s chip-wide
-                         "atomic_peak_Greq_per_s": ATOMIC_PEAK_GREQ,
-                         "atomic_frac": (round(atomics / (bwd_ms * 1e-3) / 1e9 / ATOMIC_PEAK_GREQ, 3)
-                                         if atomics else None)},
+                         "scatter": scatter},
             "kernels": {"render_fwd_ms": round(fwd_ms, 4), "render_fwd_GBs": round(fwd_gbs, 1),
                         "render_bwd_ms": round(bwd_ms, 4),
                         "path_GBs": round(value / world * PATH_BYTES_PER_RAY / 1e9, 1),
@@ -250,6 +248,15 @@ def main():
                          "parts: 3 parts in the forward (f32-accurate), 2 in the data/weight gradients"),
             "loss": round(float(loss.item()), 6),
         }
+        if scatter == "atomic" and atomics:
+            # the binding resource of the atomic scatter: memory-side float-atomic
+            # requests (TCC_EA0_ATOMIC, same PMC passes) per second, against
+            # MI355X_MICROARCH.md 'Global float atomics': ~1.3 TB/s of added bytes =
+            # 64-B memory-side requests at ~20.3 G/s chip-wide
+            rate = atomics / (bwd_ms * 1e-3) / 1e9
+            line["roofline"].update(atomic_requests=round(atomics), atomic_Greq_per_s=round(rate, 2),
+                                    atomic_peak_Greq_per_s=ATOMIC_PEAK_GREQ,
+                                    atomic_frac=round(rate / ATOMIC_PEAK_GREQ, 3))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, seconds=args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 5                 # HN_ABI_VERSION
+ABI_VERSION = 6                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -42,7 +42,7 @@ class HnMlpGrad(C.Structure):
 class HnRenderCfg(C.Structure):
     _fields_ = [("grid", HnGrid), ("n_samples", C.c_int32), ("n_importance", C.c_int32),
                 ("white_bkgd", C.c_int32), ("lindisp", C.c_int32), ("perturb", C.c_int32),
-                ("reserved", C.c_int32 * 3)]
+                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("reserved", C.c_int32)]
 
 
 _P = C.c_void_p
@@ -118,6 +118,7 @@ SIGNATURES = {
     "hn_loss_bwd": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_float, _P,
                                 _P, _P, _P, _P, _P, _P]),
     "hn_render_workspace_bytes": (C.c_size_t, [C.POINTER(HnRenderCfg), C.c_int64]),
+    "hn_render_scatter_mode": (C.c_int32, [C.POINTER(HnRenderCfg)]),
     "hn_render_fwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderFwdArgs), _P,
                                   C.c_size_t, _P]),
     "hn_render_bwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderBwdArgs), _P,

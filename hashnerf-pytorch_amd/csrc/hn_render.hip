@@ -1945,9 +1945,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     pre[threadIdx.x + 1] = inc + add;
   }
   if (threadIdx.x == 0) pre[0] = 0;
-  // bin scale: largest |value| < 2^(E+1) -> 2^40 units; overflow records may be
-  // larger (their producers' maxima are not kept): they are clamped by the
-  // same bound below, and they never occur at the sized capacities
+  // bin scale: largest |value| (overflow records included: the producer
+  // takes every record's maximum) < 2^(E+1) -> < 2^41 units
   const uint32_t bmx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
   const int E = (int)((bmx >> 23) & 0xffu) - 127;
   const double scale = ldexp(1.0, 40 - (E < -126 ? -126 : E));
@@ -1979,13 +1978,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
   for (uint32_t s = threadIdx.x; s < no; s += kBinThreads) {
     const uint32_t w = idx[ob + s];
-    if (((w & 0x0fffffffu) >> k.shift) == b) {
-      f32x4 v = vals[ob + s];
-      const float lim = (float)ldexp(1.0, E + 1);   // keep within the fixed-point range
-      v.x = fminf(fmaxf(v.x, -lim), lim); v.y = fminf(fmaxf(v.y, -lim), lim);
-      v.z = fminf(fmaxf(v.z, -lim), lim); v.w = fminf(fmaxf(v.w, -lim), lim);
-      bin_add(acc, v, w, sel, tmask, scale);
-    }
+    if (((w & 0x0fffffffu) >> k.shift) == b) bin_add(acc, vals[ob + s], w, sel, tmask, scale);
   }
   __syncthreads();
   const double inv = 1.0 / scale;
@@ -2011,6 +2004,8 @@ static int32_t check_cfg(const hn_render_cfg* c) {
   if (g.n_levels != 16 || g.n_features != 2) return HN_E_SHAPE;
   if (g.log2_hashmap_size < 1 || g.log2_hashmap_size > 24) return HN_E_SHAPE;
   if (c->n_samples != kSc || c->n_importance != kNi) return HN_E_SHAPE;
+  if (c->scatter < 0 || c->scatter > 2) return HN_E_SHAPE;
+  if (c->bin_cap < 0 || (c->bin_cap & 63)) return HN_E_SHAPE;
   return HN_OK;
 }
 
@@ -2030,26 +2025,30 @@ struct BinGeom {
   int shift, nbins, cap;
   size_t floats;
 };
-static BinGeom bin_geom(int T, int64_t n_rays) {
+static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   BinGeom g;
   g.shift = T + 4 < 13 ? T + 4 : 13;
   g.nbins = 1 << (T + 4 - g.shift);
   const double rpb = (double)((n_rays + kBwdBlocks - 1) / kBwdBlocks);
   const double avg = rpb * (kSf * 4) * ldexp(1.0, g.shift - T);
-  g.cap = (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
+  g.cap = cap_override > 0 ? cap_override : (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
   const size_t nrec = bin_records(g.nbins, g.cap);
   g.floats = nrec * 5 + (size_t)2 * kBwdBlocks * g.nbins + 4;
   return g;
 }
-// Backward schedule: HN_SCATTER = atomic (default) | split.  The split
-// scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 21).
+// Backward schedule: cfg->scatter 1 = float atomics (fused), 2 = binned
+// (split), 0 = binned unless the environment sets HN_SCATTER=atomic.  The
+// binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 21);
+// larger tables take the atomic scatter.
 static int bwd_mode(const hn_render_cfg* c) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("HN_SCATTER");
-    env = (e && !strcmp(e, "split")) ? kModeSplit : kModeAtomic;
+    env = (e && !strcmp(e, "atomic")) ? kModeAtomic : kModeSplit;
   }
-  if (env == kModeSplit && c && (16ll << c->grid.log2_hashmap_size) <= (long long)kScMaxBins << 13) return kModeSplit;
+  if (!c) return kModeAtomic;
+  const int want = c->scatter == 1 ? kModeAtomic : c->scatter == 2 ? kModeSplit : env;
+  if (want == kModeSplit && (16ll << c->grid.log2_hashmap_size) <= (long long)kScMaxBins << 13) return kModeSplit;
   return kModeAtomic;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
@@ -2063,7 +2062,7 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32 + n * (kSc + kSf) * 4;
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
-  w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays).floats : 0);
+  w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
 }
 
@@ -2076,6 +2075,10 @@ using namespace hn;
 // binned-scatter records (bin_geom) when the binned scatter is used.
 extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays) {
   return ws_layout(cfg, n_rays, bwd_mode(cfg)).total * sizeof(float);
+}
+
+extern "C" int32_t hn_render_scatter_mode(const hn_render_cfg* cfg) {
+  return bwd_mode(cfg) == kModeSplit ? 2 : 1;
 }
 
 extern "C" int32_t hn_device_faults(int32_t* faults, int32_t clear) {
@@ -2188,7 +2191,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.bin_cap = k.bin_shift = k.nbins = 0;
   k.dfeat_f = mode == kModeSplit ? (float*)workspace + wl.dfeat_f : nullptr;
   if (mode != kModeAtomic) {
-    bg = bin_geom(T, a->n_rays);
+    bg = bin_geom(T, a->n_rays, cfg->bin_cap);
     k.bins = (float*)workspace + wl.bins;
     k.bin_cap = bg.cap;
     k.bin_shift = bg.shift;

@@ -253,9 +253,10 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     return out, st
 
 
-def render_bwd(st: RenderState, grads: dict, d_table, dws):
-    """hn_render_bwd: accumulates (+=) d loss / d table into d_table and the
-    ten NeRFSmall weight gradients into dws (coarse 5, fine 5).  grads: any
+def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False):
+    """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
+    writes it, overwrite=True: d_table need not be zeroed) and the ten
+    NeRFSmall weight gradients into dws (coarse 5, fine 5, +=).  grads: any
     of g_rgb, g_depth, g_acc, g_sparsity, g_rgb0, g_depth0, g_acc0,
     g_sparsity0, g_raw_f (missing = 0)."""
     B = st.rays.shape[0]
@@ -277,6 +278,7 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws):
     a.fine_src = st.fine_src.data_ptr()
     a.feat = st.feat.data_ptr()
     a.weights_packed = 1               # same workspace and weights as the forward
+    a.d_table_mode = 1 if overwrite else 0
     a.d_coarse = L.make_mlp_grad(dws[:5])
     a.d_fine = L.make_mlp_grad(dws[5:])
     t0 = TIMER.begin("render_bwd")
@@ -506,12 +508,19 @@ def radam_step(tensors):
         L.check(L.lib().hn_radam_step(arr, len(chunk), L.stream(dev)), "radam_step")
 
 
+SCATTER_MODES = {"auto": 0, "atomic": 1, "binned": 2}
+
+
 def make_render_cfg(grid: L.HnGrid, white_bkgd: bool, lindisp: bool, perturb: bool,
-                    n_samples: int = 64, n_importance: int = 128) -> L.HnRenderCfg:
+                    n_samples: int = 64, n_importance: int = 128, scatter: str = "auto") -> L.HnRenderCfg:
+    """hn_render_cfg.  scatter: the backward's table-gradient scatter --
+    "binned" (records + exact per-bin owner pass), "atomic" (float atomics),
+    "auto" (binned unless HN_SCATTER=atomic)."""
     c = L.HnRenderCfg()
     c.grid = grid
     c.n_samples, c.n_importance = n_samples, n_importance
     c.white_bkgd, c.lindisp, c.perturb = int(white_bkgd), int(lindisp), int(perturb)
+    c.scatter = SCATTER_MODES[scatter]
     return c
 
 

@@ -366,10 +366,11 @@ class Trainer:
         lo = HF.loss_fwd(out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts)
         g_rgb, g_rgb0, g_sp, g_sp0, g_tv = HF.loss_bwd(out["rgb"], out["rgb0"], target,
                                                        0 if tv is None else tv.numel(), *consts, self._one)
-        self._gtable.zero_()
         self._gws[0]._base.zero_()                      # the ten MLP grads share one flat buffer
+        # the render backward writes every table-gradient entry (overwrite:
+        # no zero fill of the 64 MiB buffer); TV then accumulates into it
         HF.render_bwd(st, dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0),
-                      self._gtable, self._gws)
+                      self._gtable, self._gws, overwrite=True)
         if tv is not None:
             HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
         table.grad = self._gtable

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 5
+#define HN_ABI_VERSION 6
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -137,7 +137,13 @@ typedef struct hn_render_cfg {
   int32_t white_bkgd;
   int32_t lindisp;
   int32_t perturb;        /* 1: stratified jitter from t_rand */
-  int32_t reserved[3];
+  int32_t scatter;        /* backward table-gradient scatter: 0 auto (binned, unless the
+                             environment sets HN_SCATTER=atomic), 1 float atomics,
+                             2 binned (records + exact per-bin owner pass; T <= 21) */
+  int32_t bin_cap;        /* binned scatter: records per (producer block, bin) region, a
+                             multiple of 64; 0 = sized from the batch.  Small values
+                             exercise the shared overflow records (tests). */
+  int32_t reserved;
 } hn_render_cfg;
 
 #define HN_RENDER_FEAT_PER_RAY 8192   /* (64 + 192) points x 16 levels x 2 features */
@@ -266,6 +272,9 @@ int32_t hn_loss_bwd(const float* rgb, const float* rgb0, const float* target, in
                     float* g_rgb, float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv, void* stream);
 
 size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
+/* The table-gradient scatter hn_render_bwd runs for this configuration
+ * (1 float atomics, 2 binned), after cfg->scatter, HN_SCATTER and the table size. */
+int32_t hn_render_scatter_mode(const hn_render_cfg* cfg);
 int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
                       void* workspace, size_t ws_bytes, void* stream);
 int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_args* a,

@@ -1,0 +1,139 @@
+"""The backward's two table-gradient scatters against each other and their
+own properties (the embedding_dense_backward of hash_encoding.py:106 plus the
+trilinear backward, summed over the coarse and fine passes of
+run_nerf_helpers.py:538-558):
+
+* binned (records per bin + exact fixed-point owner pass) vs float atomics on
+  the same forward state: table gradients agree to 1e-6 relative norm (the
+  atomic sums are fp32 in arbitrary order, the binned sums exact), MLP
+  gradients to 1e-4 (the two schedules sum the tiles' dW in different orders);
+* the binned table gradient is bitwise reproducible (integer sums), the
+  atomic one is not required to be;
+* d_table_mode=1 (overwrite) over garbage equals += into zeros;
+* a small region capacity (cfg.bin_cap=64) pushes the hot bins' records
+  through the shared overflow records: same gradient, no device fault;
+* both against the oracle's gradient (the reference's algorithm) at
+  T=19 / finest 512 with 4096 rays, the bench shape.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BOX = (torch.tensor([-4.0, -4.0, -3.4]), torch.tensor([4.0, 4.0, 3.3]))
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float(torch.linalg.norm(a - b) / max(float(torch.linalg.norm(b)), 1e-30))
+
+
+def _state(hn, B, T, seed, scatter, bin_cap=0):
+    from importlib import import_module
+    HF = import_module("hashnerf_pytorch_amd.functional")
+    torch.manual_seed(seed)
+    emb = hn.HashEmbedder(BOX, log2_hashmap_size=T, finest_resolution=512).to(DEV)
+    with torch.no_grad():
+        emb.table.uniform_(-0.5, 0.5)
+    kw = dict(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3, hidden_dim_color=64,
+              input_ch=32, input_ch_views=16)
+    mc, mf = hn.NeRFSmall(**kw).to(DEV), hn.NeRFSmall(**kw).to(DEV)
+    focal, K = hn.rays.blender_intrinsics(400, 400)
+    ro, rd = hn.get_rays(400, 400, K, hn.pose_spherical(30.0 + seed, -30.0, 4.0)[:3, :4].to(DEV))
+    sel = torch.randperm(400 * 400, device=DEV)[:B]
+    ro, rd = ro.reshape(-1, 3)[sel], rd.reshape(-1, 3)[sel]
+    vd = rd / torch.norm(rd, dim=-1, keepdim=True)
+    rays = torch.cat([ro, rd, 2. * torch.ones_like(rd[:, :1]), 6. * torch.ones_like(rd[:, :1]), vd], -1)
+    g = torch.Generator(device=DEV).manual_seed(seed + 1)
+    t_rand = torch.rand((B, 64), device=DEV, generator=g)
+    u = torch.rand((B, 128), device=DEV, generator=g)
+    t_vals = torch.linspace(0., 1., 64, device=DEV)
+    cfg = HF.make_render_cfg(emb.grid(), True, False, True, scatter=scatter)
+    cfg.bin_cap = bin_cap
+    ws = list(mc.weights()) + list(mf.weights())
+    out, st = HF.render_fwd(cfg, rays, t_vals, t_rand, u, None, None, emb.table.detach(), ws, True)
+    target = torch.rand((B, 3), device=DEV, generator=g)
+    grads = dict(g_rgb=2. * (out["rgb"] - target) / (3 * B), g_rgb0=2. * (out["rgb0"] - target) / (3 * B),
+                 g_sparsity=torch.full((B,), 1e-3, device=DEV), g_sparsity0=torch.full((B,), 1e-3, device=DEV))
+    return HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads
+
+
+def _bwd(HF, emb, ws, st, grads, overwrite=False, init=None):
+    d_table = torch.zeros_like(emb.table) if init is None else init.clone()
+    dws = HF.zeros_like_all(ws)
+    HF.render_bwd(st, grads, d_table, dws, overwrite=overwrite)
+    torch.cuda.synchronize()
+    HF.L.check_device_faults()
+    return d_table, dws
+
+
+@pytest.mark.parametrize("T,B", [(14, 300), (19, 4096)])
+def test_binned_matches_atomic(hn, T, B):
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st_b, grads = _state(hn, B, T, 7, "binned")
+    tb, wb = _bwd(HF, emb, ws, st_b, grads)
+    *_, st_a, grads_a = _state(hn, B, T, 7, "atomic")
+    ta, wa = _bwd(HF, emb, ws, st_a, grads_a)
+    assert torch.count_nonzero(tb) > 0
+    assert _rel(tb, ta) <= 1e-6, _rel(tb, ta)
+    # same MLP backward, summed over the tiles in another order (split
+    # schedule: wave 0 coarse, waves 1-3 fine) -- fp32 summation-order level
+    for x, y in zip(wb, wa):
+        assert _rel(x, y) <= 1e-4, _rel(x, y)
+
+
+def test_binned_bitwise_reproducible_and_overwrite(hn):
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 2048, 19, 3, "binned")
+    t1, _ = _bwd(HF, emb, ws, st, grads)
+    t2, _ = _bwd(HF, emb, ws, st, grads)
+    assert torch.equal(t1, t2), "binned table gradient changed between identical launches"
+    junk = torch.full_like(emb.table, float("nan"))
+    t3, _ = _bwd(HF, emb, ws, st, grads, overwrite=True, init=junk)
+    assert torch.equal(t1, t3), "d_table_mode=1 must overwrite every entry"
+    base = torch.randn_like(emb.table)
+    t4, _ = _bwd(HF, emb, ws, st, grads, init=base)
+    assert torch.equal(t4, base + t1), "d_table_mode=0 adds the gradient once"
+
+
+def test_binned_overflow_records(hn):
+    """cap 64 per (block, bin) region (sized: 256): the regions of the hot
+    coarse-level bins of a 1024-ray batch spill into the shared overflow
+    records; the owner pass picks them up."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 1024, 19, 5, "binned")
+    t_full, _ = _bwd(HF, emb, ws, st, grads)
+    *_, st_small, grads_small = _state(hn, 1024, 19, 5, "binned", bin_cap=64)
+    t_small, _ = _bwd(HF, emb, ws, st_small, grads_small)
+    assert _rel(t_small, t_full) <= 1e-6, _rel(t_small, t_full)
+
+
+def test_binned_vs_oracle_bench_shape(hn, oracle):
+    """T=19, finest 512, 4096 rays (BASELINE configs[1] shape): the binned
+    table and MLP gradients against the oracle on a 32-ray subset of the
+    loss (rays are independent, so the subset's gradient is exact)."""
+    O = oracle
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, _ = _state(hn, 4096, 19, 11, "binned")
+    n = 32
+    sub = torch.randperm(4096, generator=torch.Generator().manual_seed(4))[:n].to(DEV)
+    cfg = HF.make_render_cfg(emb.grid(), True, False, True, scatter="binned")
+    fo, st = HF.render_fwd(cfg, rays, torch.linspace(0., 1., 64, device=DEV), t_rand, u, None, None,
+                           emb.table.detach(), ws, True)
+    g_rgb = torch.zeros((4096, 3), device=DEV)
+    g_rgb0 = torch.zeros((4096, 3), device=DEV)
+    g_rgb[sub] = 2. * (fo["rgb"][sub] - target[sub])
+    g_rgb0[sub] = 2. * (fo["rgb0"][sub] - target[sub])
+    d_table, dws = _bwd(HF, emb, ws, st, dict(g_rgb=g_rgb, g_rgb0=g_rgb0))
+    tab = emb.table.detach().cpu().requires_grad_(True)
+    wc = {k: v.detach().cpu().requires_grad_(True) for k, v in zip(O.MLP_KEYS, mc.weights())}
+    wf = {k: v.detach().cpu().requires_grad_(True) for k, v in zip(O.MLP_KEYS, mf.weights())}
+    ret = O.render_rays(rays[sub].cpu(), wc, wf, tab, BOX[0], BOX[1], O.level_resolutions(16, 16, 512), 19,
+                        t_rand=t_rand[sub].cpu(), u=u[sub].cpu(), white_bkgd=True,
+                        z_fine=fo["z_fine"][sub].cpu())
+    same = np.isclose(fo["z_fine"][sub].cpu().numpy(), ret["z_vals"].detach().numpy(), rtol=0, atol=1e-5)
+    assert same.mean() > 0.97, f"only {same.mean():.4f} of fine samples agree"
+    ref = ((ret["rgb_map"] - target[sub].cpu()) ** 2).sum() + ((ret["rgb0"] - target[sub].cpu()) ** 2).sum()
+    ref.backward()
+    assert _rel(d_table, tab.grad) <= 5e-4, _rel(d_table, tab.grad)
+    for p, w_ref in ((dws[:5], wc), (dws[5:], wf)):
+        for x, k in zip(p, O.MLP_KEYS):
+            assert _rel(x, w_ref[k].grad) <= 5e-4, (k, _rel(x, w_ref[k].grad))
