@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 6                 # HN_ABI_VERSION
+ABI_VERSION = 7                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -57,13 +57,22 @@ class HnRenderFwdArgs(C.Structure):
                 ("fine_src", _P), ("feat", _P)]
 
 
+class HnRadamTensor(C.Structure):
+    _fields_ = [("p", _P), ("g", _P), ("m", _P), ("v", _P), ("n", C.c_int64),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("one_minus_beta1", C.c_float),
+                ("one_minus_beta2", C.c_float), ("eps", C.c_float), ("neg_wd_lr", C.c_float),
+                ("neg_step_lr", C.c_float), ("mode", C.c_int32), ("has_wd", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 class HnRenderBwdArgs(C.Structure):
     _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("noise_c", _P), ("noise_f", _P), ("table", _P),
                 ("coarse", HnMlp), ("fine", HnMlp), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P),
                 ("raw_f", _P), ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32),
                 ("d_table_mode", C.c_int32), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
-                ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad)]
+                ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
+                ("table_step", C.POINTER(HnRadamTensor))]
 
 
 class HnTvArgs(C.Structure):
@@ -80,13 +89,6 @@ class HnRaySampler(C.Structure):
                 ("cx", C.c_float), ("cy", C.c_float), ("near", C.c_float), ("far", C.c_float),
                 ("seed", C.c_uint64)]
 
-
-class HnRadamTensor(C.Structure):
-    _fields_ = [("p", _P), ("g", _P), ("m", _P), ("v", _P), ("n", C.c_int64),
-                ("beta1", C.c_float), ("beta2", C.c_float), ("one_minus_beta1", C.c_float),
-                ("one_minus_beta2", C.c_float), ("eps", C.c_float), ("neg_wd_lr", C.c_float),
-                ("neg_step_lr", C.c_float), ("mode", C.c_int32), ("has_wd", C.c_int32),
-                ("reserved", C.c_int32)]
 
 
 # name -> (restype, argtypes); must match include/hashnerf_amd.h exactly.
@@ -118,7 +120,7 @@ SIGNATURES = {
     "hn_loss_bwd": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_float, _P,
                                 _P, _P, _P, _P, _P, _P]),
     "hn_render_workspace_bytes": (C.c_size_t, [C.POINTER(HnRenderCfg), C.c_int64]),
-    "hn_render_scatter_mode": (C.c_int32, [C.POINTER(HnRenderCfg)]),
+    "hn_render_scatter_mode": (C.c_int32, [C.POINTER(HnRenderCfg), C.c_int64]),
     "hn_render_fwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderFwdArgs), _P,
                                   C.c_size_t, _P]),
     "hn_render_bwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderBwdArgs), _P,

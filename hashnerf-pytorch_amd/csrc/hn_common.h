@@ -134,6 +134,20 @@ HN_DEV void trilerp_bwd(float g, const float w[3], float out[8]) {
   }
 }
 
+// RAdam per element (radam.py:58-92) in the op forms of torch's CPU kernels
+// (verified bit-exact on the reference's RAdam trace, tests/golden/radam.npz):
+// add_(x, alpha) = fma(alpha, x, self); addcmul_ = fma(value * t1, t2, self);
+// addcdiv_ = self + (value * t1) / t2.
+HN_DEV void radam_elem(const hn_radam_tensor& d, float& p, float g, float& m, float& v) {
+  v = __builtin_fmaf(d.one_minus_beta2 * g, g, v * d.beta2);   // exp_avg_sq.mul_(b2).addcmul_
+  m = __builtin_fmaf(d.one_minus_beta1, g, m * d.beta1);       // exp_avg.mul_(b1).add_
+  if (d.mode != 0) {
+    if (d.has_wd) p = __builtin_fmaf(d.neg_wd_lr, p, p);      // p.add_(-wd*lr, p)
+    if (d.mode == 2) p = p + (d.neg_step_lr * m) / (sqrtf(v) + d.eps);   // addcdiv_
+    else p = __builtin_fmaf(d.neg_step_lr, m, p);              // add_(-step_size*lr, exp_avg)
+  }
+}
+
 HN_DEV void atomic_add_f32(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -231,6 +245,13 @@ HN_DEV double shfl_from(double v, int src) {
 
 HN_DEV uint32_t shfl_from(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
+HN_DEV float wave_max_f32(float v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = fmaxf(v, __int_as_float(__builtin_amdgcn_ds_bpermute((l ^ d) << 2, __float_as_int(v))));
+  return v;
 }
 
 template <typename T>

@@ -112,19 +112,6 @@ struct RadamK {
   hn_radam_tensor t[HN_RADAM_MAX_TENSORS];
 };
 
-// Op forms of torch's CPU kernels (verified bit-exact on the reference's RAdam
-// trace, tests/golden/radam.npz): add_(x, alpha) = fma(alpha, x, self);
-// addcmul_ = fma(value * t1, t2, self); addcdiv_ = self + (value * t1) / t2.
-HN_DEV void radam_elem(const hn_radam_tensor& d, float& p, float g, float& m, float& v) {
-  v = __builtin_fmaf(d.one_minus_beta2 * g, g, v * d.beta2);   // exp_avg_sq.mul_(b2).addcmul_
-  m = __builtin_fmaf(d.one_minus_beta1, g, m * d.beta1);       // exp_avg.mul_(b1).add_
-  if (d.mode != 0) {
-    if (d.has_wd) p = __builtin_fmaf(d.neg_wd_lr, p, p);      // p.add_(-wd*lr, p)
-    if (d.mode == 2) p = p + (d.neg_step_lr * m) / (sqrtf(v) + d.eps);   // addcdiv_
-    else p = __builtin_fmaf(d.neg_step_lr, m, p);              // add_(-step_size*lr, exp_avg)
-  }
-}
-
 __global__ __launch_bounds__(256) void radam_kernel(RadamK k) {
   const hn_radam_tensor& d = k.t[blockIdx.y];
   const int64_t n = d.n;

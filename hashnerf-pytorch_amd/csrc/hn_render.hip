@@ -1121,12 +1121,11 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // <= 11 for cells <= 1024, so both rows fall in one 2^13-entry bin).
 // Layout (floats from bins): vals f32x4 [nbins][kBwdBlocks][cap] (a bin's
 // regions are contiguous for its owner) then kOvfRecs overflow records; idx
-// u32 over the same record index; counts u32 [nbins][kBwdBlocks]; max |value|
-// bits u32 [nbins][kBwdBlocks]; overflow count.  The producer counts its
-// records per bin in LDS (ds_add_rtn) and keeps the bin's largest |value|
-// (ds_max_u32 on the float bits: the owner's fixed-point scale); a full region
-// spills to the shared overflow records (one returning global atomic each,
-// rare by sizing).
+// u32 over the same record index; counts u32 [nbins][kBwdBlocks]; largest
+// |value| per level f32 [16][kBwdBlocks] (the owner's fixed-point scale);
+// overflow count.  The producer counts its records per bin in LDS
+// (ds_add_rtn); a full region spills to the shared overflow records (one
+// returning global atomic each, rare by sizing).
 constexpr int kOvfRecs = 1 << 20;
 enum : int { kFaultBins = 16 };
 
@@ -1134,11 +1133,10 @@ struct BinW {
   f32x4* vals;
   uint32_t* idx;
   uint32_t* lcnt;      // LDS [nbins] record counts
-  uint32_t* lmax;      // LDS [nbins] largest |value| bits
   uint32_t* ovf_cnt;
-  size_t base;         // first record of this block's region of bin 0
-  size_t stride;       // records between a block's regions of consecutive bins
-  size_t ovf_base;     // first overflow record
+  uint32_t base;       // first record of this block's region of bin 0
+  uint32_t stride;     // records between a block's regions of consecutive bins
+  uint32_t ovf_base;   // first overflow record
   uint32_t cap, shift;
 };
 
@@ -1172,28 +1170,64 @@ HN_DEV void seg_sum4(float (&v)[4], uint32_t pm, int pp, bool s1, bool s2, bool 
 }
 
 // A run head's record: the x-pair (x0 = cx, x1 = cx + 1) of corner row (yy, zz)
-// (the y / z coordinates times their primes) at level l.
-HN_DEV void emit_record(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx, uint32_t yy, uint32_t zz,
-                        const float (&v)[4]) {
+// (the y / z coordinates times their primes) at level l.  rec_slot takes the
+// record's slot in its bin (LDS counter); rec_store writes it -- split so a
+// caller can have several counter round trips in flight.
+struct RecSlot {
+  uint32_t word, bin, slot;
+};
+HN_DEV RecSlot rec_slot(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx, uint32_t yy, uint32_t zz) {
   const uint32_t mask = (1u << log2T) - 1u;
   const uint32_t flat = (l << log2T) + ((cx ^ yy ^ zz) & mask);
   const uint32_t nbits = (uint32_t)__builtin_ctz(~cx) + 1u;
-  const uint32_t bin = flat >> bw.shift;
-  const uint32_t mx = max(max(__float_as_uint(v[0]) & 0x7fffffffu, __float_as_uint(v[1]) & 0x7fffffffu),
-                          max(__float_as_uint(v[2]) & 0x7fffffffu, __float_as_uint(v[3]) & 0x7fffffffu));
-  __hip_atomic_fetch_max(bw.lmax + bin, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const uint32_t slot = __hip_atomic_fetch_add(bw.lcnt + bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  size_t r = bw.base + (size_t)bin * bw.stride + slot;
+  RecSlot r;
+  r.word = flat | (nbits << 28);
+  r.bin = flat >> bw.shift;
+#if HN_SC_DIAG == 2   // diagnostic: no counter round trip (wrong records)
+  r.slot = cx & 7u;
+#else
+  r.slot = __hip_atomic_fetch_add(bw.lcnt + r.bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+  return r;
+}
+HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
+  // record index < 2^28 (bwd_mode keeps the buffer under 4 GiB): 32-bit byte
+  // offsets from a uniform base
+  uint32_t r = bw.base + rs.bin * bw.stride + rs.slot;
   bool ok = true;
-  if (slot >= bw.cap) {
+  if (rs.slot >= bw.cap) {
     const uint32_t o = __hip_atomic_fetch_add(bw.ovf_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ok = o < (uint32_t)kOvfRecs;
     r = bw.ovf_base + o;
     if (!ok) __hip_atomic_fetch_or(&g_hn_fault, kFaultBins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#if HN_SC_DIAG >= 1   // diagnostic: no record stores (wrong gradient)
+  ok = ok && v[0] == 1234.5f && v[1] == 5432.1f;
+#endif
   if (ok) {
-    bw.vals[r] = f32x4{v[0], v[1], v[2], v[3]};
-    bw.idx[r] = flat | (nbits << 28);
+    *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(bw.vals) + r * 16u) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(bw.idx) + r * 4u) = rs.word;
+  }
+}
+
+// Voxel of one (point, level) for the split scatter: the cell is the IEEE
+// quotient's floor (the forward's), taken from num * RN(1/g) when that product
+// is farther than its error bound (1.5 ulp, doubled) from an integer, else
+// from the division itself; the weights are the reference's IEEE divisions.
+HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], const float xc[3], int l,
+                        int32_t cell[3], float w[3]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float gs = gsl[3 * l + a];
+    const float num = xc[a] - g.bmin[a];
+    float q = num * gsl[kGsRcp + 3 * l + a];
+    const float fq = floorf(q), fr = q - fq;
+    const float tol = fmaxf(q, 1.f) * 0x1p-21f;
+    const int32_t i = (fr < tol || fr > 1.f - tol) ? (int32_t)floorf(num / gs) : (int32_t)fq;
+    const float vmin = (float)i * gs + g.bmin[a];
+    const float vmax = vmin + gs;
+    w[a] = (pt[a] - vmin) / (vmax - vmin);
+    cell[a] = i;
   }
 }
 
@@ -1206,6 +1240,15 @@ HN_DEV void emit_record(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx,
 // level; per corner row the x-pair sums over runs of samples in one voxel
 // (16-lane rows, as in the fused scatter) and one record per run head.  Block
 // b is producer b of the record layout (kBwdBlocks blocks).
+#ifndef HN_SC_FASTCELL   // 1: cell from num * RN(1/g) with an exact fallback (voxel_cw_sc)
+#define HN_SC_FASTCELL 1
+#endif
+#ifndef HN_SC_BATCH      // 1: the 4 corner rows' slot round trips before their stores
+#define HN_SC_BATCH 1
+#endif
+#ifndef HN_SC_DIAG       // diagnostics (wrong gradients): 1 no record stores, 2 also no slot counters
+#define HN_SC_DIAG 0
+#endif
 struct ScK {
   GridArgs g;
   int64_t B;
@@ -1221,22 +1264,23 @@ constexpr int kScWaves = 16;
 constexpr int kScMaxBins = 4096;   // LDS counters + maxima (32 KiB): T <= 21 at 2^13 entries per bin
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
-  __shared__ uint32_t bcnt[kScMaxBins], bmax[kScMaxBins];
-  __shared__ float gsl[kGsLds];
+  __shared__ uint32_t bcnt[kScMaxBins];
+  __shared__ float gsl[kGsLds], lvmx[16];
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = bmax[i] = 0u;
+  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
+  if (threadIdx.x < 16) lvmx[threadIdx.x] = 0.f;
   stage_grid_sizes(k.g, gsl);
   __syncthreads();
   BinW bw;
   const size_t nrec = bin_records(k.nbins, k.bin_cap);
   bw.vals = reinterpret_cast<f32x4*>(k.bins);
   bw.idx = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
-  bw.ovf_cnt = bw.idx + nrec + (size_t)2 * kBwdBlocks * k.nbins;
+  bw.ovf_cnt = bw.idx + nrec + (size_t)kBwdBlocks * (k.nbins + 16);
   bw.lcnt = bcnt;
-  bw.lmax = bmax;
-  bw.base = (size_t)blockIdx.x * k.bin_cap;
-  bw.stride = (size_t)kBwdBlocks * k.bin_cap;
-  bw.ovf_base = (size_t)kBwdBlocks * k.nbins * k.bin_cap;
+  bw.base = blockIdx.x * (uint32_t)k.bin_cap;
+  bw.stride = kBwdBlocks * (uint32_t)k.bin_cap;
+  bw.ovf_base = kBwdBlocks * (uint32_t)k.nbins * (uint32_t)k.bin_cap;
+
   bw.cap = (uint32_t)k.bin_cap;
   bw.shift = (uint32_t)k.bin_shift;
   const int64_t units = 3 * k.B;
@@ -1282,7 +1326,11 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     for (int l = 0; l < 16; ++l) {
       int32_t cell[3];
       float w[3];
+#if HN_SC_FASTCELL
+      voxel_cw_sc(k.g, gsl, pt, xc, l, cell, w);
+#else
       voxel_cw(k.g, gsl, pt, xc, l, cell, w);
+#endif
       const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
       const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
       const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
@@ -1295,25 +1343,36 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
       // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
       const float gz[2][2] = {{g0 * az, g1 * az}, {g0 * w[2], g1 * w[2]}};   // [k][f]
+      float vmax = 0.f;   // largest |record value| of the level: the owner's fixed-point scale
+      float v[4][4];
+      RecSlot rs[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < 4; ++c) {   // sums and slots of the 4 corner rows: 4 counter round trips in flight
         const int j = c >> 1, kk = c & 1;
         const float wy = j ? w[1] : ay;
         const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
-        float v[4] = {a0 * ax, a1 * ax, a0 * w[0], a1 * w[0]};
-        seg_sum4(v, pm, pp, s1, s2, s4, s8);
-        if (head) emit_record(bw, (uint32_t)l, (uint32_t)k.g.log2T, cx, j ? y0 + kPrimeY : y0,
-                              kk ? z0 + kPrimeZ : z0, v);
+        v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
+        seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
+        vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+        if (head) rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)k.g.log2T, cx, j ? y0 + kPrimeY : y0,
+                                   kk ? z0 + kPrimeZ : z0);
+        if (!HN_SC_BATCH && head) rec_store(bw, rs[c], v[c]);
       }
+      if (HN_SC_BATCH && head) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rec_store(bw, rs[c], v[c]);
+      }
+      vmax = wave_max_f32(vmax);
+      if (lane == 0)
+        __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   __syncthreads();
   uint32_t* cnt = bw.idx + nrec + blockIdx.x;
-  uint32_t* mxo = cnt + (size_t)kBwdBlocks * k.nbins;
-  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
-    cnt[(size_t)i * kBwdBlocks] = bcnt[i];
-    mxo[(size_t)i * kBwdBlocks] = bmax[i];
-  }
+  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) cnt[(size_t)i * kBwdBlocks] = bcnt[i];
+  float* mxo = reinterpret_cast<float*>(bw.idx + nrec + (size_t)kBwdBlocks * k.nbins) + blockIdx.x;
+  if (threadIdx.x < 16) mxo[threadIdx.x * kBwdBlocks] = lvmx[threadIdx.x];
 }
 
 // The table-gradient scatter of one slot (embedding_dense_backward of
@@ -1612,7 +1671,7 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0 && threadIdx.x == 0) {   // binned scatter: no overflow records yet
     const size_t nrec = bin_records(k.nbins, k.bin_cap);
-    reinterpret_cast<uint32_t*>(k.bins + 4 * nrec)[nrec + (size_t)2 * kBwdBlocks * k.nbins] = 0u;
+    reinterpret_cast<uint32_t*>(k.bins + 4 * nrec)[nrec + (size_t)kBwdBlocks * (k.nbins + 16)] = 0u;
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -1882,29 +1941,38 @@ __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const flo
 struct BinR {
   const float* bins;
   int32_t nbins, cap, shift, log2T;
-  float* d_table;
+  float* d_table;          // or NULL (fused step only)
   int32_t overwrite;
+  int32_t fused;           // 1: apply `step` to the table (p, m, v) with the bin's gradient
+  hn_radam_tensor step;
 };
 constexpr int kBinThreads = 1024;
+#ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
+#define HN_BR_DIAG 0
+#endif
 
-HN_DEV uint32_t wave_max_u32(uint32_t v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v = max(v, shfl_from(v, lane ^ d));
-  return v;
+// round(v * 2^S) as int64 without f64 arithmetic: x = v * 2^S is exact in fp32
+// (|x| < 2^41, a power-of-2 scale), a = trunc(x / 2^16) is an exact integer,
+// b = x - a * 2^16 exact with |b| < 2^16, and round(x) = a * 2^16 + rint(b)
+// (ties to even agree: a * 2^16 is even).
+HN_DEV long long fx_of(float v, float scale) {
+  const float x = v * scale;
+  const float a = truncf(x * 0x1p-16f);
+  const float b = __builtin_fmaf(-a, 0x1p16f, x);
+  return ((long long)(int32_t)a << 16) + (long long)(int32_t)rintf(b);
 }
 
-HN_DEV long long fx_of(float v, double scale) { return __double2ll_rn((double)v * scale); }
-
-HN_DEV void bin_add(unsigned long long* acc, const f32x4 v, uint32_t w, uint32_t sel, uint32_t tmask,
-                    double scale) {
+// acc: [feature][entry] (entry e's accumulators 8 B apart per feature: a
+// wave's random entries spread over twice the LDS banks of [entry][feature])
+HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_t w, uint32_t sel,
+                    uint32_t tmask, float scale) {
   const uint32_t e0 = w & 0x0fffffffu & sel;
   const uint32_t e1 = e0 ^ (((1u << (w >> 28)) - 1u) & tmask);
   const long long q[4] = {fx_of(v.x, scale), fx_of(v.y, scale), fx_of(v.z, scale), fx_of(v.w, scale)};
-  __hip_atomic_fetch_add(acc + 2 * e0, (unsigned long long)q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_add(acc + 2 * e0 + 1, (unsigned long long)q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_add(acc + 2 * e1, (unsigned long long)q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_add(acc + 2 * e1 + 1, (unsigned long long)q[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + e0, (unsigned long long)q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + se + e0, (unsigned long long)q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + e1, (unsigned long long)q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(acc + se + e1, (unsigned long long)q[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Records of the bin, flattened over the producers' regions: thread i takes
@@ -1923,17 +1991,21 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   const f32x4* vals = reinterpret_cast<const f32x4*>(k.bins);
   const uint32_t* idx = reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec);
   const uint32_t* cnt = idx + nrec;
-  const uint32_t* mxs = cnt + (size_t)kBwdBlocks * k.nbins;
-  const uint32_t n_ovf = mxs[(size_t)kBwdBlocks * k.nbins];
+  const float* mxs = reinterpret_cast<const float*>(cnt + (size_t)kBwdBlocks * k.nbins);   // [16][blocks]
+  const uint32_t n_ovf = cnt[(size_t)kBwdBlocks * (k.nbins + 16)];
   static_assert(kBwdBlocks == 256 && kBinThreads >= 256, "one count per thread of waves 0-3");
-  uint32_t n = 0, mx = 0;
+  // levels of this bin: one, or all 16 when the whole table is one bin
+  const int lev0 = (int)(((uint32_t)b << k.shift) >> k.log2T);
+  const int nlev = k.shift > k.log2T ? 1 << (k.shift - k.log2T) : 1;
+  uint32_t n = 0;
+  float mx = 0.f;
   if (threadIdx.x < kBwdBlocks) {
     const uint32_t c = cnt[(size_t)b * kBwdBlocks + threadIdx.x];
     n = c < (uint32_t)k.cap ? c : (uint32_t)k.cap;
-    mx = mxs[(size_t)b * kBwdBlocks + threadIdx.x];
+    for (int l = lev0; l < lev0 + nlev; ++l) mx = fmaxf(mx, mxs[l * kBwdBlocks + threadIdx.x]);
   }
   const uint32_t inc = (uint32_t)wave_incl_sum((double)n);   // exact: counts < 2^53
-  const uint32_t wmx = wave_max_u32(mx);
+  const float wmx = wave_max_f32(mx);
   if (threadIdx.x < kBwdBlocks && (threadIdx.x & 63) == 63) {
     wsum[threadIdx.x >> 6] = inc;
     wmax[threadIdx.x >> 6] = wmx;
@@ -1945,18 +2017,23 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     pre[threadIdx.x + 1] = inc + add;
   }
   if (threadIdx.x == 0) pre[0] = 0;
-  // bin scale: largest |value| (overflow records included: the producer
-  // takes every record's maximum) < 2^(E+1) -> < 2^41 units
-  const uint32_t bmx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-  const int E = (int)((bmx >> 23) & 0xffu) - 127;
-  const double scale = ldexp(1.0, 40 - (E < -126 ? -126 : E));
+  // bin scale: every record value (overflow records included: the producers
+  // take every record) is below 2^(E+1) -> below 2^41 units
+  const float bmx = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  const int E = ilogbf(bmx > 0.f ? bmx : 1.f);
+  // 2^(40 - E) as fp32 (E >= -126 + ... : the scale stays a normal float for
+  // every E in [-87, 127]; smaller maxima use 2^127, still < 2^41 units)
+  const int S = 40 - (E < -126 ? -126 : E);
+  const float scale = ldexpf(1.f, S > 127 ? 127 : S);
   __syncthreads();
   const uint32_t total = pre[kBwdBlocks];
-  const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u;
+  const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u, se = 1u << k.shift;
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
-  for (uint32_t r0 = threadIdx.x; r0 < total; r0 += 4 * kBinThreads) {
-    f32x4 v[4];
-    uint32_t w[4];
+  // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found by
+  // a binary search over the regions' prefix (measured faster than one search
+  // per 4 lane-consecutive records with their 64-B-strided loads); the next
+  // 4 records are loaded before the current ones are added (8 in flight)
+  auto fetch = [&](uint32_t r0, f32x4 (&v)[4], uint32_t (&w)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t r = r0 + q * kBinThreads;
@@ -1970,31 +2047,72 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
         w[q] = idx[rec];
       }
     }
+  };
+  f32x4 va[4], vb[4];
+  uint32_t wa[4], wb[4];
+  uint32_t r0 = threadIdx.x;
+  if (r0 < total) fetch(r0, va, wa);
+  for (; r0 < total; r0 += 8 * kBinThreads) {
+    const uint32_t r1 = r0 + 4 * kBinThreads;
+    if (r1 < total) fetch(r1, vb, wb);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (r0 + q * kBinThreads < total) bin_add(acc, v[q], w[q], sel, tmask, scale);
+      if (r0 + q * kBinThreads < total) {
+#if HN_BR_DIAG == 1   // diagnostic: record loads only
+        if (va[q].x == 1234.5f && wa[q] == 7u) acc[threadIdx.x] = 1ull;
+#else
+        bin_add(acc, se, va[q], wa[q], sel, tmask, scale);
+#endif
+      }
+    if (r1 >= total) break;
+    if (r1 + 4 * kBinThreads < total) fetch(r1 + 4 * kBinThreads, va, wa);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (r1 + q * kBinThreads < total) {
+#if HN_BR_DIAG == 1
+        if (vb[q].x == 1234.5f && wb[q] == 7u) acc[threadIdx.x] = 1ull;
+#else
+        bin_add(acc, se, vb[q], wb[q], sel, tmask, scale);
+#endif
+      }
   }
   const uint32_t no = n_ovf < (uint32_t)kOvfRecs ? n_ovf : (uint32_t)kOvfRecs;
   const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
   for (uint32_t s = threadIdx.x; s < no; s += kBinThreads) {
     const uint32_t w = idx[ob + s];
-    if (((w & 0x0fffffffu) >> k.shift) == b) bin_add(acc, vals[ob + s], w, sel, tmask, scale);
+    if (((w & 0x0fffffffu) >> k.shift) == b) bin_add(acc, se, vals[ob + s], w, sel, tmask, scale);
   }
   __syncthreads();
-  const double inv = 1.0 / scale;
-  float4* dst = reinterpret_cast<float4*>(k.d_table + ((size_t)b << (k.shift + 1)));
+  const double inv = 1.0 / (double)scale;
+  const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
+  float4* dst = k.d_table ? reinterpret_cast<float4*>(k.d_table + e0) : nullptr;
   const int nd4 = (2 << k.shift) / 4;
-  for (int i = threadIdx.x; i < nd4; i += kBinThreads) {
+  for (int i = threadIdx.x; i < nd4; i += kBinThreads) {   // entries 2i, 2i + 1
     float4 a;
-    a.x = (float)((double)(long long)acc[4 * i] * inv);
-    a.y = (float)((double)(long long)acc[4 * i + 1] * inv);
-    a.z = (float)((double)(long long)acc[4 * i + 2] * inv);
-    a.w = (float)((double)(long long)acc[4 * i + 3] * inv);
-    if (!k.overwrite) {
-      const float4 d = dst[i];
-      a.x = a.x + d.x; a.y = a.y + d.y; a.z = a.z + d.z; a.w = a.w + d.w;
+    a.x = (float)((double)(long long)acc[2 * i] * inv);
+    a.y = (float)((double)(long long)acc[se + 2 * i] * inv);
+    a.z = (float)((double)(long long)acc[2 * i + 1] * inv);
+    a.w = (float)((double)(long long)acc[se + 2 * i + 1] * inv);
+    if (dst) {
+      if (!k.overwrite) {
+        const float4 d = dst[i];
+        a.x = a.x + d.x; a.y = a.y + d.y; a.z = a.z + d.z; a.w = a.w + d.w;
+      }
+      dst[i] = a;
     }
-    dst[i] = a;
+    if (k.fused) {   // RAdam on these 4 table elements (radam_kernel's update, same op forms)
+      float4* pp = reinterpret_cast<float4*>(k.step.p + e0) + i;
+      float4* mp = reinterpret_cast<float4*>(k.step.m + e0) + i;
+      float4* vp = reinterpret_cast<float4*>(k.step.v + e0) + i;
+      float4 p = *pp, m = *mp, v = *vp;
+      radam_elem(k.step, p.x, a.x, m.x, v.x);
+      radam_elem(k.step, p.y, a.y, m.y, v.y);
+      radam_elem(k.step, p.z, a.z, m.z, v.z);
+      radam_elem(k.step, p.w, a.w, m.w, v.w);
+      *mp = m;
+      *vp = v;
+      if (k.step.mode != 0) *pp = p;
+    }
   }
 }
 
@@ -2033,14 +2151,14 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   const double avg = rpb * (kSf * 4) * ldexp(1.0, g.shift - T);
   g.cap = cap_override > 0 ? cap_override : (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
   const size_t nrec = bin_records(g.nbins, g.cap);
-  g.floats = nrec * 5 + (size_t)2 * kBwdBlocks * g.nbins + 4;
+  g.floats = nrec * 5 + (size_t)kBwdBlocks * (g.nbins + 16) + 4;
   return g;
 }
 // Backward schedule: cfg->scatter 1 = float atomics (fused), 2 = binned
 // (split), 0 = binned unless the environment sets HN_SCATTER=atomic.  The
 // binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 21);
 // larger tables take the atomic scatter.
-static int bwd_mode(const hn_render_cfg* c) {
+static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("HN_SCATTER");
@@ -2048,8 +2166,10 @@ static int bwd_mode(const hn_render_cfg* c) {
   }
   if (!c) return kModeAtomic;
   const int want = c->scatter == 1 ? kModeAtomic : c->scatter == 2 ? kModeSplit : env;
-  if (want == kModeSplit && (16ll << c->grid.log2_hashmap_size) <= (long long)kScMaxBins << 13) return kModeSplit;
-  return kModeAtomic;
+  if (want != kModeSplit || (16ll << c->grid.log2_hashmap_size) > (long long)kScMaxBins << 13) return kModeAtomic;
+  // the producers address records with 32-bit byte offsets
+  const BinGeom g = bin_geom(c->grid.log2_hashmap_size, n_rays, c->bin_cap);
+  return bin_records(g.nbins, g.cap) * 16 < (1ull << 32) ? kModeSplit : kModeAtomic;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
 // coarse-pass feature grads [n][64][32] | d raw [n][256][4] | split: fine
@@ -2074,11 +2194,11 @@ using namespace hn;
 // coarse-pass feature grads [n_rays][64][32] | d raw [n_rays][256][4] |
 // binned-scatter records (bin_geom) when the binned scatter is used.
 extern "C" size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays) {
-  return ws_layout(cfg, n_rays, bwd_mode(cfg)).total * sizeof(float);
+  return ws_layout(cfg, n_rays, bwd_mode(cfg, n_rays)).total * sizeof(float);
 }
 
-extern "C" int32_t hn_render_scatter_mode(const hn_render_cfg* cfg) {
-  return bwd_mode(cfg) == kModeSplit ? 2 : 1;
+extern "C" int32_t hn_render_scatter_mode(const hn_render_cfg* cfg, int64_t n_rays) {
+  return bwd_mode(cfg, n_rays) == kModeSplit ? 2 : 1;
 }
 
 extern "C" int32_t hn_device_faults(int32_t* faults, int32_t clear) {
@@ -2150,7 +2270,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (!a->rays || !a->table || !mlp_ok(a->coarse) || !mlp_ok(a->fine)) return HN_E_NULL;
   if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f || !a->fine_src || !a->feat)
     return HN_E_NULL;
-  if (!a->d_table || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
+  if ((!a->d_table && !a->table_step) || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
   if (a->d_table_mode != 0 && a->d_table_mode != 1) return HN_E_SHAPE;
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
@@ -2184,7 +2304,12 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.fine_src = a->fine_src;
   k.d_table = a->d_table;
   const int T = cfg->grid.log2_hashmap_size;
-  const int mode = bwd_mode(cfg);
+  const int mode = bwd_mode(cfg, a->n_rays);
+  if (a->table_step) {   // the fused step lives in the binned scatter's owner pass
+    const hn_radam_tensor& ts = *a->table_step;
+    if (mode != kModeSplit || ts.n != ((int64_t)16 << cfg->grid.log2_hashmap_size) * 2) return HN_E_SHAPE;
+    if (!ts.p || !ts.m || !ts.v) return HN_E_NULL;
+  }
   const WsLayout wl = ws_layout(cfg, a->n_rays, mode);
   BinGeom bg{};
   k.bins = nullptr;
@@ -2239,6 +2364,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.log2T = T;
     r.d_table = a->d_table;
     r.overwrite = a->d_table_mode == 1;
+    r.fused = a->table_step != nullptr;
+    if (r.fused) r.step = *a->table_step;
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
                        (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
     if ((st = hip_status(hipGetLastError()))) return st;

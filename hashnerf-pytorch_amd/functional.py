@@ -7,6 +7,7 @@ the kernels, mirroring the C ABI contract.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 from typing import Optional, Sequence
 
@@ -253,12 +254,14 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     return out, st
 
 
-def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False):
+def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=).  grads: any
     of g_rgb, g_depth, g_acc, g_sparsity, g_rgb0, g_depth0, g_acc0,
-    g_sparsity0, g_raw_f (missing = 0)."""
+    g_sparsity0, g_raw_f (missing = 0).  table_step = (table, exp_avg,
+    exp_avg_sq, coeffs) from RAdam.take_step: the binned owner pass applies
+    that RAdam step to the table with this gradient (d_table may be None)."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -272,6 +275,8 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
             ("rays", st.rays), ("noise_c", st.noise_c), ("noise_f", st.noise_f), ("table", st.table),
             ("z_coarse", st.z_c), ("z_fine", st.z_f), ("raw_c", st.raw_c), ("raw_f", st.raw_f),
             ("d_table", d_table)]:
+        if t is not None and k == "d_table" and not t.is_contiguous():
+            raise RuntimeError("hashnerf_amd.render_bwd: d_table must be contiguous")
         t = L.contig(t)
         keep.append(t)
         setattr(a, k, None if t is None else t.data_ptr())
@@ -281,6 +286,17 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     a.d_table_mode = 1 if overwrite else 0
     a.d_coarse = L.make_mlp_grad(dws[:5])
     a.d_fine = L.make_mlp_grad(dws[5:])
+    step = None
+    if table_step is not None:
+        p, m, v, c = table_step
+        L.require_device(p, m, v)
+        step = L.HnRadamTensor()
+        step.p, step.g, step.m, step.v = p.data_ptr(), None, m.data_ptr(), v.data_ptr()
+        step.n = p.numel()
+        for k in ("beta1", "beta2", "one_minus_beta1", "one_minus_beta2", "eps", "neg_wd_lr", "neg_step_lr",
+                  "mode", "has_wd"):
+            setattr(step, k, c[k])
+        a.table_step = C.pointer(step)
     t0 = TIMER.begin("render_bwd")
     L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
     TIMER.end("render_bwd", t0)

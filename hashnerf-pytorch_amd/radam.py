@@ -55,33 +55,54 @@ class RAdam(Optimizer):
         buffered[2] = step_size
         return n_sma, step_size
 
+    def _prepare(self, group, p):
+        """Advance p's step and return its (exp_avg, exp_avg_sq, coeffs)."""
+        beta1, beta2 = group["betas"]
+        state = self.state[p]
+        if len(state) == 0:
+            state["step"] = 0
+            state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        state["step"] += 1
+        n_sma, step_size = self._coeffs(group, state["step"])
+        mode = 2 if n_sma >= 5 else (1 if step_size > 0 else 0)
+        lr, wd = group["lr"], group["weight_decay"]
+        c = {"beta1": beta1, "beta2": beta2, "one_minus_beta1": 1 - beta1,
+             "one_minus_beta2": 1 - beta2, "eps": group["eps"], "neg_wd_lr": -wd * lr,
+             "neg_step_lr": -step_size * lr if mode else 0.0, "mode": mode,
+             "has_wd": int(wd != 0)}
+        return state["exp_avg"], state["exp_avg_sq"], c
+
+    @torch.no_grad()
+    def take_step(self, p):
+        """Hand p's next update to a fused kernel: advances p's state exactly
+        as step() would and returns (p, exp_avg, exp_avg_sq, coeffs) for
+        functional.render_bwd(table_step=...); the next step() leaves p
+        alone.  Call it at the point of the iteration where step() would run
+        for p (same lr)."""
+        for group in self.param_groups:
+            if any(q is p for q in group["params"]):
+                m, v, c = self._prepare(group, p)
+                self._fused = getattr(self, "_fused", set()) | {id(p)}
+                return p, m, v, c
+        raise ValueError("RAdam.take_step: not a parameter of this optimizer")
+
     @torch.no_grad()
     def step(self, closure=None):
-        """All parameters of all groups in one HIP launch (hn_radam_step)."""
+        """All parameters of all groups in one HIP launch (hn_radam_step);
+        parameters handed to take_step since the last step() are skipped."""
         loss = closure() if closure is not None else None
         work = []
+        fused, self._fused = getattr(self, "_fused", set()), set()
         for group in self.param_groups:
-            beta1, beta2 = group["betas"]
             for p in group["params"]:
-                if p.grad is None:
+                if id(p) in fused or p.grad is None:
                     continue
                 grad = p.grad
                 if grad.is_sparse:
                     raise RuntimeError("RAdam does not support sparse gradients")
-                state = self.state[p]
-                if len(state) == 0:
-                    state["step"] = 0
-                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                state["step"] += 1
-                n_sma, step_size = self._coeffs(group, state["step"])
-                mode = 2 if n_sma >= 5 else (1 if step_size > 0 else 0)
-                lr, wd = group["lr"], group["weight_decay"]
-                c = {"beta1": beta1, "beta2": beta2, "one_minus_beta1": 1 - beta1,
-                     "one_minus_beta2": 1 - beta2, "eps": group["eps"], "neg_wd_lr": -wd * lr,
-                     "neg_step_lr": -step_size * lr if mode else 0.0, "mode": mode,
-                     "has_wd": int(wd != 0)}
-                work.append((p, grad.contiguous(), state["exp_avg"], state["exp_avg_sq"], c))
+                m, v, c = self._prepare(group, p)
+                work.append((p, grad.contiguous(), m, v, c))
         if work:
             HF.radam_step(work)
         return loss

@@ -269,6 +269,9 @@ class Trainer:
         # every this many steps: one blocking copy, so a failed internal wait
         # can never leave silently wrong gradients behind for long
         self.fault_check_every = 100
+        # explicit mode, one GPU: fuse the table's RAdam step into the binned
+        # backward's owner pass when the step has no TV term
+        self.fuse_table_step = True
 
     def sample_rays(self, i: int):
         """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
@@ -318,6 +321,7 @@ class Trainer:
         self._ws = nf.weights() + nfine.weights()
         table = self.embed_fn.table
         self._gtable = torch.zeros_like(table)
+        self._binned = HF.L.lib().hn_render_scatter_mode(self._cfg, a.N_rand) == 2
         self._gws = HF.zeros_like_all(self._ws)
         self._one = torch.ones((), device=self.device)
         self._grads = True
@@ -367,13 +371,21 @@ class Trainer:
         g_rgb, g_rgb0, g_sp, g_sp0, g_tv = HF.loss_bwd(out["rgb"], out["rgb0"], target,
                                                        0 if tv is None else tv.numel(), *consts, self._one)
         self._gws[0]._base.zero_()                      # the ten MLP grads share one flat buffer
-        # the render backward writes every table-gradient entry (overwrite:
-        # no zero fill of the 64 MiB buffer); TV then accumulates into it
-        HF.render_bwd(st, dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0),
-                      self._gtable, self._gws, overwrite=True)
-        if tv is not None:
-            HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
-        table.grad = self._gtable
+        grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)
+        if self.fuse_table_step and self.world == 1 and tv is None and self._binned:
+            # one GPU, no TV term: the table gradient is complete where the
+            # binned owner pass forms it, so the table's RAdam step runs there
+            # (run_nerf.py:642 for the embedding group) and the gradient is
+            # never stored; optimizer.step() then updates the MLP groups only
+            HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table))
+            table.grad = None
+        else:
+            # the render backward writes every table-gradient entry (overwrite:
+            # no zero fill of the 64 MiB buffer); TV then accumulates into it
+            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True)
+            if tv is not None:
+                HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
+            table.grad = self._gtable
         for p, g in zip(self._ws, self._gws):
             p.grad = g
         return lo[0], lo[1]

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 6
+#define HN_ABI_VERSION 7
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -192,8 +192,14 @@ typedef struct hn_render_bwd_args {
   const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;
   const float* g_raw_f;     /* [B][192][4] or NULL */
   /* gradient outputs (+=) */
-  float* d_table;           /* [16][2^T][2] */
+  float* d_table;           /* [16][2^T][2]; may be NULL when table_step is given */
   hn_mlp_grad d_coarse; hn_mlp_grad d_fine;
+  /* Optional fused optimizer step (binned scatter only, else HN_E_SHAPE): the
+   * owner pass applies this RAdam step (hn_radam_step's per-element update,
+   * g = the table gradient of this backward) to the table right where it forms
+   * the gradient; p / m / v are the table and its moments, g is ignored.
+   * NULL = no step (the gradient goes to d_table). */
+  const struct hn_radam_tensor* table_step;
 } hn_render_bwd_args;
 
 /* ---- L4 hash-table total variation (loss.py:11-43), all levels at once ---
@@ -272,9 +278,10 @@ int32_t hn_loss_bwd(const float* rgb, const float* rgb0, const float* target, in
                     float* g_rgb, float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv, void* stream);
 
 size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
-/* The table-gradient scatter hn_render_bwd runs for this configuration
- * (1 float atomics, 2 binned), after cfg->scatter, HN_SCATTER and the table size. */
-int32_t hn_render_scatter_mode(const hn_render_cfg* cfg);
+/* The table-gradient scatter hn_render_bwd runs for this configuration and
+ * batch (1 float atomics, 2 binned), after cfg->scatter, HN_SCATTER, the
+ * table size and the record buffer size. */
+int32_t hn_render_scatter_mode(const hn_render_cfg* cfg, int64_t n_rays);
 int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
                       void* workspace, size_t ws_bytes, void* stream);
 int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_args* a,

@@ -137,3 +137,29 @@ def test_binned_vs_oracle_bench_shape(hn, oracle):
     for p, w_ref in ((dws[:5], wc), (dws[5:], wf)):
         for x, k in zip(p, O.MLP_KEYS):
             assert _rel(x, w_ref[k].grad) <= 5e-4, (k, _rel(x, w_ref[k].grad))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_fused_table_step_bitwise(hn, mode):
+    """The RAdam step fused into the owner pass (render_bwd(table_step=...))
+    equals hn_radam_step on the gradient the same backward writes, bitwise,
+    in each of RAdam's three update forms (radam.py:58-92: moments only while
+    N_sma < 5 and step_size < 0, the SGD-like form, the rectified form)."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 2048, 19, 9, "binned")
+    g = torch.Generator(device=DEV).manual_seed(5)
+    p0 = emb.table.detach().clone()
+    m0 = torch.randn(p0.shape, device=DEV, generator=g) * 1e-6
+    v0 = torch.rand(p0.shape, device=DEV, generator=g) * 1e-10
+    c = {"beta1": 0.9, "beta2": 0.99, "one_minus_beta1": 1 - 0.9, "one_minus_beta2": 1 - 0.99, "eps": 1e-15,
+         "neg_wd_lr": 0.0, "neg_step_lr": -0.0421 * 0.01 if mode else 0.0, "mode": mode, "has_wd": 0}
+    pf, mf_, vf = p0.clone(), m0.clone(), v0.clone()
+    dws = HF.zeros_like_all(ws)
+    HF.render_bwd(st, grads, None, dws, table_step=(pf, mf_, vf, c))
+    d_table, _ = _bwd(HF, emb, ws, st, grads)
+    pr, mr, vr = p0.clone(), m0.clone(), v0.clone()
+    HF.radam_step([(pr, d_table, mr, vr, c)])
+    torch.cuda.synchronize()
+    assert torch.equal(mf_, mr) and torch.equal(vf, vr)
+    assert torch.equal(pf, pr)
+    if mode:
+        assert not torch.equal(pf, p0)
