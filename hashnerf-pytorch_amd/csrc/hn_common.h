@@ -349,6 +349,26 @@ HN_DEV f32x16 mfma_split(const SP<NS>& a, const SP<NS>& b, f32x16 c) {
   c = mfma_bf(a.p[0], b.p[1], c);
   return mfma_bf(a.p[0], b.p[0], c);
 }
+// c0 += A0 . B, c1 += A1 . B (one split of B, the two chains interleaved;
+// each accumulator sees the products in mfma_split's order)
+template <int NS>
+HN_DEV void mfma_split2(const SP<NS>& a0, const SP<NS>& a1, const SP<NS>& b, f32x16& c0, f32x16& c1) {
+  static_assert(NS == 2 || NS == 3, "parts");
+  if constexpr (NS == 3) {
+    c0 = mfma_bf(a0.p[2], b.p[0], c0);
+    c1 = mfma_bf(a1.p[2], b.p[0], c1);
+    c0 = mfma_bf(a0.p[0], b.p[2], c0);
+    c1 = mfma_bf(a1.p[0], b.p[2], c1);
+    c0 = mfma_bf(a0.p[1], b.p[1], c0);
+    c1 = mfma_bf(a1.p[1], b.p[1], c1);
+  }
+  c0 = mfma_bf(a0.p[1], b.p[0], c0);
+  c1 = mfma_bf(a1.p[1], b.p[0], c1);
+  c0 = mfma_bf(a0.p[0], b.p[1], c0);
+  c1 = mfma_bf(a1.p[0], b.p[1], c1);
+  c0 = mfma_bf(a0.p[0], b.p[0], c0);
+  c1 = mfma_bf(a1.p[0], b.p[0], c1);
+}
 // Level handled by register pair (2m, 2m+1) of lane half h in the 32-feature
 // tile layout: feature ROW(2m,h) = 2 * lev(m,h).
 HN_DEV constexpr int tile_level(int m, int h) { return (m & 1) + 4 * (m >> 1) + 2 * h; }

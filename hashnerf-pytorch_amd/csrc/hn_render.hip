@@ -417,6 +417,9 @@ HN_DEV void put_rows(float* X, int row0, const f32x16& v, int lane) {
 
 // acc[n][k] += sum over the tile's 32 points of A[arow_n][pt] * B[brow_k][pt];
 // arow / brow are this lane's rows (n = k = lane & 31).
+#ifndef HN_WGRAD_SHARE   // 1: wgrad_n splits each LDS operand row once per chunk
+#define HN_WGRAD_SHARE 1
+#endif
 HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
   const int h = lane >> 5;
   const f32x4* pa = reinterpret_cast<const f32x4*>(X + arow * kXS + 16 * h);
@@ -447,37 +450,91 @@ HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
   return acc;
 }
 
+// acc[NB * a + b] += wgrad(X, arow[a], brow[b]): each operand row is read and
+// split once per chunk for all the blocks that use it
+template <int NA, int NB>
+HN_DEV void wgrad_n(const float* X, const int (&arow)[NA], const int (&brow)[NB], f32x16* acc, int lane) {
+#if HN_SPLIT_W && HN_WGRAD_SHARE
+  const int h = lane >> 5;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    SP<HN_SPLIT_W> a[NA], b[NB];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const f32x4* pa = reinterpret_cast<const f32x4*>(X + arow[j] * kXS + 16 * h);
+      a[j] = splitn<HN_SPLIT_W>(pa[2 * c], pa[2 * c + 1]);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const f32x4* pb = reinterpret_cast<const f32x4*>(X + brow[j] * kXS + 16 * h);
+      b[j] = splitn<HN_SPLIT_W>(pb[2 * c], pb[2 * c + 1]);
+    }
+#pragma unroll
+    for (int ja = 0; ja < NA; ++ja)
+#pragma unroll
+      for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = mfma_split<HN_SPLIT_W>(a[ja], b[jb], acc[NB * ja + jb]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#else
+#pragma unroll
+  for (int ja = 0; ja < NA; ++ja)
+#pragma unroll
+    for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = wgrad(X, arow[ja], brow[jb], acc[NB * ja + jb], lane);
+#endif
+}
+
 // ---- weight-fragment stream ----------------------------------------------
 // A tile's 15 data-path GEMMs read their packed A-fragment groups (one 1-KiB
 // dwordx4 load per wave: 4 f32 k-steps, or one bf16 part of 8 k-steps) in a
 // fixed order (92 groups at HN_SPLIT_F = 3, HN_SPLIT_B = 2), padded to a
-// multiple of the ring depth so that the ring lines up with the tile period.  The ring keeps the next 4
-// groups (16 MFMAs, ~1000 cycles) in flight across GEMM, tile and unit
-// boundaries: no GEMM starts on an exposed L2 latency at one wave per SIMD.
+// multiple of the ring depth so that the ring lines up with the tile period.
+// The ring keeps the next 8 groups (~16 bf16 MFMAs with their splits) in
+// flight across GEMM, tile and unit boundaries: no GEMM starts on an exposed
+// L2 latency at one wave per SIMD.  Depth 4 measured 484 us for the config-2
+// MLP backward, 8: 460 us.  The two output blocks of a GEMM are paired
+// (kSegs, gemm_w2): one B split per chunk for both, two independent
+// accumulator chains (515 -> 484 us together with wgrad_n's shared splits).
 struct GemmSeg {
-  int r, ob;   // region (hn_mlp.h), output block
+  int r, ob;   // region (hn_mlp.h), output block; ob = -1: both blocks, chunk by chunk
 };
+#ifndef HN_PAIR_OB   // 1: the two output blocks of a GEMM share one B split (gemm_w2)
+#define HN_PAIR_OB 1
+#endif
+#if HN_PAIR_OB
+constexpr GemmSeg kSegs[] = {{R_F0, -1}, {R_F1, 0}, {R_F2G, -1}, {R_F3, -1}, {R_B4, -1},
+                             {R_B3, -1}, {R_B2G, 0}, {R_B1, -1}, {R_B0, 0}};
+#else
 constexpr GemmSeg kSegs[] = {{R_F0, 0}, {R_F0, 1}, {R_F1, 0}, {R_F2G, 0}, {R_F2G, 1}, {R_F3, 0}, {R_F3, 1},
                              {R_B4, 0}, {R_B4, 1}, {R_B3, 0}, {R_B3, 1}, {R_B2G, 0}, {R_B1, 0}, {R_B1, 1},
                              {R_B0, 0}};
+#endif
 constexpr int kNSegs = sizeof(kSegs) / sizeof(kSegs[0]);
+constexpr int seg_groups(const GemmSeg& g) { return reg_gpo(g.r) * (g.ob < 0 ? 2 : 1); }
 constexpr int seg_start(int i) {   // first group of segment i in the stream
   int n = 0;
-  for (int j = 0; j < i; ++j) n += reg_gpo(kSegs[j].r);
+  for (int j = 0; j < i; ++j) n += seg_groups(kSegs[j]);
   return n;
 }
 #ifndef HN_WRING
-#define HN_WRING 4
+#define HN_WRING 8
 #endif
 constexpr int kTileGroups = seg_start(kNSegs), kRing = HN_WRING;
 constexpr int kTilePeriod = (kTileGroups + kRing - 1) / kRing * kRing;   // pad groups keep slots static
+// A paired segment streams chunk c of block 0 (its NS groups; f32: one
+// group), then chunk c of block 1, then chunk c + 1 ...
 constexpr int group_off(int idx) {
   idx %= kTilePeriod;
   if (idx >= kTileGroups) idx = 0;              // pad groups re-read group 0
   for (const GemmSeg& g : kSegs) {
     const int n = reg_gpo(g.r);
-    if (idx < n) return reg_off(g.r) + (g.ob * n + idx) * 256;
-    idx -= n;
+    if (g.ob >= 0) {
+      if (idx < n) return reg_off(g.r) + (g.ob * n + idx) * 256;
+    } else if (idx < 2 * n) {
+      const int per = reg_ns(g.r) ? reg_ns(g.r) : 1;   // groups per chunk and block
+      const int c = idx / (2 * per), ob = idx / per % 2, q = idx % per;
+      return reg_off(g.r) + (ob * n + per * c + q) * 256;
+    }
+    idx -= seg_groups(g);
   }
   return 0;
 }
@@ -543,6 +600,81 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
   return acc;
 }
 
+// acc0 / acc1 += blocks 0 / 1 of the paired segment SEG . B: one B split per
+// chunk for both blocks, and two independent accumulator chains
+#ifndef HN_W2_SWP   // 1: software-pipelined B splits (diagnostic A/B)
+#define HN_W2_SWP 0
+#endif
+template <int SEG, typename BF>
+HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int lane, BF bval) {
+  constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = reg_ns(R), START = seg_start(SEG);
+  static_assert(kSegs[SEG].ob < 0, "paired segment");
+  if constexpr (NS > 0) {
+    constexpr int NC = KS / 8;
+#if HN_W2_SWP
+    SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
+#endif
+    static_for<0, NC>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      SP<NS> a0, a1;
+      static_for<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        a0.p[q] = as_bf16x8(wring_take<START + 2 * NS * c + q>(w, P, lane));
+      });
+      static_for<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        a1.p[q] = as_bf16x8(wring_take<START + 2 * NS * c + NS + q>(w, P, lane));
+      });
+#if HN_W2_SWP
+      // the next chunk's B split (VALU) runs in this chunk's MFMA shadow
+      SP<NS> bn = b;
+      if constexpr (c + 1 < NC) bn = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
+      mfma_split2<NS>(a0, a1, b, acc0, acc1);
+      if constexpr (c + 1 < NC) {
+        static_for<0, 2 * (NS == 3 ? 6 : 3)>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // then up to 4 VALU
+        });
+      }
+      b = bn;
+#else
+      const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
+      mfma_split2<NS>(a0, a1, b, acc0, acc1);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  } else {
+    static_for<0, KS / 4>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      const f32x4 a0 = wring_take<START + 2 * g>(w, P, lane);
+      const f32x4 a1 = wring_take<START + 2 * g + 1>(w, P, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc0 = mfma(a0[j], bval(4 * g + j), acc0);
+        acc1 = mfma(a1[j], bval(4 * g + j), acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+}
+
+constexpr int seg_of(int r) {   // first stream segment of region r
+  for (int i = 0; i < kNSegs; ++i)
+    if (kSegs[i].r == r) return i;
+  return -1;
+}
+// acc[0..1] += both output blocks of region R . B
+template <int R, typename BF>
+HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval) {
+  constexpr int S = seg_of(R);
+  if constexpr (kSegs[S].ob < 0) {
+    gemm_w2<S>(w, P, acc[0], acc[1], lane, bval);
+  } else {
+    acc[0] = gemm_w<S>(w, P, acc[0], lane, bval);
+    acc[1] = gemm_w<S + 1>(w, P, acc[1], lane, bval);
+  }
+}
+
 HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -564,33 +696,31 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
   // ---- forward recompute (models.py:151-174) ----
   put_rows(X, kRF, feat, lane);
-  f32x16 h0[2];
-  h0[0] = gemm_w<0>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
+  f32x16 h0[2] = {zero16(), zero16()};
+  gemm2<R_F0>(wr, P, h0, lane, [&](int s) { return feat[s]; });
   relu_bits(h0[0], mh0, 0);
-  put_rows(X, kRH0, h0[0], lane);
-  h0[1] = gemm_w<1>(wr, P, zero16(), lane, [&](int s) { return feat[s]; });
   relu_bits(h0[1], mh0, 1);
+  put_rows(X, kRH0, h0[0], lane);
   put_rows(X, kRH0 + 32, h0[1], lane);
-  const f32x16 s1 = gemm_w<2>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
+  const f32x16 s1 = gemm_w<seg_of(R_F1)>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
 #pragma unroll
   for (int r = 0; r < 8; ++r) {                 // geo rows 1..15 -> image rows 16..30
     const int row = row_of(r, h);
     if (row >= 1) X[(kRC0in + 15 + row) * kXS + p] = s1[r];
   }
-  f32x16 c0[2];
-  c0[0] = gemm_w<3>(wr, P, c0sh[0], lane, [&](int s) { return s1[s]; });
+  f32x16 c0[2] = {c0sh[0], c0sh[1]};
+  gemm2<R_F2G>(wr, P, c0, lane, [&](int s) { return s1[s]; });
   relu_bits(c0[0], mc0, 0);
-  put_rows(X, kRC0, c0[0], lane);
-  c0[1] = gemm_w<4>(wr, P, c0sh[1], lane, [&](int s) { return s1[s]; });
   relu_bits(c0[1], mc0, 1);
+  put_rows(X, kRC0, c0[0], lane);
   put_rows(X, kRC0 + 32, c0[1], lane);
   {
-    f32x16 c1 = gemm_w<5>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
-    relu_bits(c1, mc1, 0);
-    put_rows(X, kRC1, c1, lane);
-    c1 = gemm_w<6>(wr, P, zero16(), lane, [&](int s) { return c0[s >> 4][s & 15]; });
-    relu_bits(c1, mc1, 1);
-    put_rows(X, kRC1 + 32, c1, lane);
+    f32x16 c1[2] = {zero16(), zero16()};
+    gemm2<R_F3>(wr, P, c1, lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    relu_bits(c1[0], mc1, 0);
+    relu_bits(c1[1], mc1, 1);
+    put_rows(X, kRC1, c1[0], lane);
+    put_rows(X, kRC1 + 32, c1[1], lane);
   }
   if (h == 0) {
     X[(kRC2 + 0) * kXS + p] = dr.x;
@@ -600,12 +730,13 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   lds_fence_wave();
   // ---- color_net.2 ----
   const int rc2 = kRC2 + (i < 3 ? i : 3);       // rows >= 3 of this block are discarded
-  dw.c2[0] = wgrad(X, rc2, kRC1 + i, dw.c2[0], lane);
-  dw.c2[1] = wgrad(X, rc2, kRC1 + 32 + i, dw.c2[1], lane);
+  {
+    const int ar[1] = {rc2}, br[2] = {kRC1 + i, kRC1 + 32 + i};
+    wgrad_n<1, 2>(X, ar, br, dw.c2, lane);
+  }
   const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
-  f32x16 dc1[2];
-  dc1[0] = gemm_w<7>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
-  dc1[1] = gemm_w<8>(wr, P, zero16(), lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
+  f32x16 dc1[2] = {zero16(), zero16()};
+  gemm2<R_B4>(wr, P, dc1, lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
   mask_bits(dc1[0], mc1, 0);
   mask_bits(dc1[1], mc1, 1);
   lds_fence_wave();
@@ -613,42 +744,45 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   put_rows(X, kRC1, dc1[0], lane);
   put_rows(X, kRC1 + 32, dc1[1], lane);
   lds_fence_wave();
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-      dw.c1[2 * nb + kb] = wgrad(X, kRC1 + 32 * nb + i, kRC0 + 32 * kb + i, dw.c1[2 * nb + kb], lane);
-  f32x16 dc0[2];
-  dc0[0] = gemm_w<9>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+  {
+    const int ar[2] = {kRC1 + i, kRC1 + 32 + i}, br[2] = {kRC0 + i, kRC0 + 32 + i};
+    wgrad_n<2, 2>(X, ar, br, dw.c1, lane);     // dw.c1[2 * nb + kb]
+  }
+  f32x16 dc0[2] = {zero16(), zero16()};
+  gemm2<R_B3>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; });
   mask_bits(dc0[0], mc0, 0);
-  dc0[1] = gemm_w<10>(wr, P, zero16(), lane, [&](int s) { return dc1[s >> 4][s & 15]; });
   mask_bits(dc0[1], mc0, 1);
   lds_fence_wave();
   // ---- color_net.0: X = [sh16 | geo15] (dc0 image over the c0 rows) ----
   put_rows(X, kRC0, dc0[0], lane);
   put_rows(X, kRC0 + 32, dc0[1], lane);
   lds_fence_wave();
-  dw.c0[0] = wgrad(X, kRC0 + i, kRC0in + i, dw.c0[0], lane);
-  dw.c0[1] = wgrad(X, kRC0 + 32 + i, kRC0in + i, dw.c0[1], lane);
-  f32x16 ds1 = gemm_w<11>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+  {
+    const int ar[2] = {kRC0 + i, kRC0 + 32 + i}, br[1] = {kRC0in + i};
+    wgrad_n<2, 1>(X, ar, br, dw.c0, lane);
+  }
+  f32x16 ds1 = gemm_w<seg_of(R_B2G)>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
   // ---- sigma_net.1 (ds1 image over the c1 rows; rows 16..31 are zero) ----
   put_rows(X, kRC1, ds1, lane);
   lds_fence_wave();
-  dw.s1[0] = wgrad(X, kRC1 + i, kRH0 + i, dw.s1[0], lane);
-  dw.s1[1] = wgrad(X, kRC1 + i, kRH0 + 32 + i, dw.s1[1], lane);
-  f32x16 dh0[2];
-  dh0[0] = gemm_w<12>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
-  dh0[1] = gemm_w<13>(wr, P, zero16(), lane, [&](int s) { return ds1[s]; });
+  {
+    const int ar[1] = {kRC1 + i}, br[2] = {kRH0 + i, kRH0 + 32 + i};
+    wgrad_n<1, 2>(X, ar, br, dw.s1, lane);
+  }
+  f32x16 dh0[2] = {zero16(), zero16()};
+  gemm2<R_B1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; });
   mask_bits(dh0[0], mh0, 0);
   mask_bits(dh0[1], mh0, 1);
   // ---- sigma_net.0 (dh0 image over the c0 rows) ----
   put_rows(X, kRC0, dh0[0], lane);
   put_rows(X, kRC0 + 32, dh0[1], lane);
   lds_fence_wave();
-  dw.s0[0] = wgrad(X, kRC0 + i, kRF + i, dw.s0[0], lane);
-  dw.s0[1] = wgrad(X, kRC0 + 32 + i, kRF + i, dw.s0[1], lane);
-  const f32x16 dfeat = gemm_w<14>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  {
+    const int ar[2] = {kRC0 + i, kRC0 + 32 + i}, br[1] = {kRF + i};
+    wgrad_n<2, 1>(X, ar, br, dw.s0, lane);
+  }
+  const f32x16 dfeat = gemm_w<seg_of(R_B0)>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
   static_for<kTileGroups, kTilePeriod - kTileGroups>([&](auto gc) {   // pad groups: keep the ring
     (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
   });
@@ -1120,28 +1254,58 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // x1 = x0 + 1 differs from x0 in its trailing ones and the bit above (nbits
 // <= 11 for cells <= 1024, so both rows fall in one 2^13-entry bin).
 // Layout (floats from bins): vals f32x4 [nbins][kBwdBlocks][cap] (a bin's
-// regions are contiguous for its owner) then kOvfRecs overflow records; idx
-// u32 over the same record index; counts u32 [nbins][kBwdBlocks]; largest
-// |value| per level f32 [16][kBwdBlocks] (the owner's fixed-point scale);
-// overflow count.  The producer counts its records per bin in LDS
-// (ds_add_rtn); a full region spills to the shared overflow records (one
-// returning global atomic each, rare by sizing).
-constexpr int kOvfRecs = 1 << 20;
+// regions are contiguous for its owner) then the overflow lists
+// [kBwdBlocks][ovf_per_block]; idx u32 over the same record index; counts u32
+// [nbins][kBwdBlocks]; largest |value| per level f32 [16][kBwdBlocks] (the
+// owner's fixed-point scale); then the overflow book (OvfBook).  The producer
+// counts its records per bin in LDS (ds_add_rtn); a record past its region's
+// capacity goes to the block's own overflow list (one more LDS counter), so
+// spilling costs no global atomic.  A block's list holds every record the
+// block can make (64 samples x 16 levels x 4 corner rows per unit): clumped
+// input (a scene box inside the sample range, where every out-of-box sample
+// clamps onto the box surface; the coarse levels of a T = 22 table) spills
+// but never runs out.  ovf_place_kernel buckets the spilled records by bin so
+// that each owner reads only its own.
 enum : int { kFaultBins = 16 };
 
 struct BinW {
   f32x4* vals;
   uint32_t* idx;
   uint32_t* lcnt;      // LDS [nbins] record counts
-  uint32_t* ovf_cnt;
-  uint32_t base;       // first record of this block's region of bin 0
-  uint32_t stride;     // records between a block's regions of consecutive bins
-  uint32_t ovf_base;   // first overflow record
+  uint32_t* lovf;      // LDS: this block's overflow records
+  size_t base;         // first record of this block's region of bin 0
+  size_t stride;       // records between a block's regions of consecutive bins
+  size_t ovf_base;     // first record of this block's overflow list
+  uint32_t n_ovf;      // its length
   uint32_t cap, shift;
 };
 
-__host__ __device__ inline size_t bin_records(int nbins, int cap) {
-  return (size_t)kBwdBlocks * nbins * cap + kOvfRecs;
+__host__ __device__ inline int64_t sc_units_per_block(int64_t n_rays) {   // scatter_bins_kernel: 3 units per ray
+  return (3 * (n_rays > 0 ? n_rays : 1) + kBwdBlocks - 1) / kBwdBlocks;
+}
+__host__ __device__ inline size_t ovf_per_block(int64_t n_rays) { return (size_t)sc_units_per_block(n_rays) * 64 * 64; }
+__host__ __device__ inline size_t bin_records(int nbins, int cap, int64_t n_rays) {
+  return (size_t)kBwdBlocks * nbins * cap + (size_t)kBwdBlocks * ovf_per_block(n_rays);
+}
+// Overflow book, u32 words after the counts and level maxima (idx + nrec +
+// kBwdBlocks * (nbins + 16)): total spilled, spilled per bin, placement
+// cursors, first slot per bin, spilled per producer block, record ids
+// (relative to the first overflow record) bucketed by bin.
+struct OvfBook {
+  uint32_t *cnt, *per_bin, *cur, *first, *blk, *ids;
+};
+__host__ __device__ inline size_t ovf_book_words(int nbins, int64_t n_rays) {
+  return 1 + 3 * (size_t)nbins + kBwdBlocks + (size_t)kBwdBlocks * ovf_per_block(n_rays);
+}
+__host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbins) {
+  OvfBook o;
+  o.cnt = idx + nrec + (size_t)kBwdBlocks * (nbins + 16);
+  o.per_bin = o.cnt + 1;
+  o.cur = o.per_bin + nbins;
+  o.first = o.cur + nbins;
+  o.blk = o.first + nbins;
+  o.ids = o.blk + kBwdBlocks;
+  return o;
 }
 
 // Segmented suffix sum over runs of samples in one voxel along a 16-lane
@@ -1191,13 +1355,11 @@ HN_DEV RecSlot rec_slot(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx,
   return r;
 }
 HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
-  // record index < 2^28 (bwd_mode keeps the buffer under 4 GiB): 32-bit byte
-  // offsets from a uniform base
-  uint32_t r = bw.base + rs.bin * bw.stride + rs.slot;
+  size_t r = bw.base + (size_t)rs.bin * bw.stride + rs.slot;
   bool ok = true;
   if (rs.slot >= bw.cap) {
-    const uint32_t o = __hip_atomic_fetch_add(bw.ovf_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ok = o < (uint32_t)kOvfRecs;
+    const uint32_t o = __hip_atomic_fetch_add(bw.lovf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    ok = o < bw.n_ovf;   // always, by the list's size
     r = bw.ovf_base + o;
     if (!ok) __hip_atomic_fetch_or(&g_hn_fault, kFaultBins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1205,8 +1367,8 @@ HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
   ok = ok && v[0] == 1234.5f && v[1] == 5432.1f;
 #endif
   if (ok) {
-    *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(bw.vals) + r * 16u) = f32x4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(bw.idx) + r * 4u) = rs.word;
+    bw.vals[r] = f32x4{v[0], v[1], v[2], v[3]};
+    bw.idx[r] = rs.word;
   }
 }
 
@@ -1261,25 +1423,29 @@ struct ScK {
   int32_t bin_cap, bin_shift, nbins;
 };
 constexpr int kScWaves = 16;
-constexpr int kScMaxBins = 4096;   // LDS counters + maxima (32 KiB): T <= 21 at 2^13 entries per bin
+constexpr int kScMaxBins = 8192;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __shared__ uint32_t bcnt[kScMaxBins];
   __shared__ float gsl[kGsLds], lvmx[16];
+  __shared__ uint32_t lovf;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
   if (threadIdx.x < 16) lvmx[threadIdx.x] = 0.f;
+  if (threadIdx.x == 0) lovf = 0u;
   stage_grid_sizes(k.g, gsl);
   __syncthreads();
   BinW bw;
-  const size_t nrec = bin_records(k.nbins, k.bin_cap);
+  const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
   bw.vals = reinterpret_cast<f32x4*>(k.bins);
   bw.idx = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
-  bw.ovf_cnt = bw.idx + nrec + (size_t)kBwdBlocks * (k.nbins + 16);
+  const OvfBook ob = ovf_book(bw.idx, nrec, k.nbins);
+  bw.lovf = &lovf;
+  bw.n_ovf = (uint32_t)ovf_per_block(k.B);
   bw.lcnt = bcnt;
-  bw.base = blockIdx.x * (uint32_t)k.bin_cap;
-  bw.stride = kBwdBlocks * (uint32_t)k.bin_cap;
-  bw.ovf_base = kBwdBlocks * (uint32_t)k.nbins * (uint32_t)k.bin_cap;
+  bw.base = (size_t)blockIdx.x * k.bin_cap;
+  bw.stride = (size_t)kBwdBlocks * k.bin_cap;
+  bw.ovf_base = (size_t)kBwdBlocks * k.nbins * k.bin_cap + (size_t)blockIdx.x * bw.n_ovf;
 
   bw.cap = (uint32_t)k.bin_cap;
   bw.shift = (uint32_t)k.bin_shift;
@@ -1370,9 +1536,19 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
   __syncthreads();
   uint32_t* cnt = bw.idx + nrec + blockIdx.x;
-  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) cnt[(size_t)i * kBwdBlocks] = bcnt[i];
+  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
+    const uint32_t c = bcnt[i];
+    cnt[(size_t)i * kBwdBlocks] = c;
+    if (c > bw.cap)   // spilled records of bin i (ovf_place_kernel's bucket sizes)
+      __hip_atomic_fetch_add(ob.per_bin + i, c - bw.cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   float* mxo = reinterpret_cast<float*>(bw.idx + nrec + (size_t)kBwdBlocks * k.nbins) + blockIdx.x;
   if (threadIdx.x < 16) mxo[threadIdx.x * kBwdBlocks] = lvmx[threadIdx.x];
+  if (threadIdx.x == 0) {
+    const uint32_t n = lovf < bw.n_ovf ? lovf : bw.n_ovf;
+    ob.blk[blockIdx.x] = n;
+    if (n) __hip_atomic_fetch_add(ob.cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // The table-gradient scatter of one slot (embedding_dense_backward of
@@ -1669,9 +1845,10 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   __shared__ float lds[kFwdWaves][kSf * 5];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  if (k.bins && blockIdx.x == 0 && threadIdx.x == 0) {   // binned scatter: no overflow records yet
-    const size_t nrec = bin_records(k.nbins, k.bin_cap);
-    reinterpret_cast<uint32_t*>(k.bins + 4 * nrec)[nrec + (size_t)kBwdBlocks * (k.nbins + 16)] = 0u;
+  if (k.bins && blockIdx.x == 0) {   // binned scatter: no overflow records yet (count, per bin, cursors)
+    const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
+    uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
+    for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -1940,6 +2117,7 @@ __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const flo
 // either once a larger contribution has been added.
 struct BinR {
   const float* bins;
+  int64_t n_rays;
   int32_t nbins, cap, shift, log2T;
   float* d_table;          // or NULL (fused step only)
   int32_t overwrite;
@@ -1975,6 +2153,67 @@ HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_
   __hip_atomic_fetch_add(acc + se + e1, (unsigned long long)q[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Buckets the spilled records by bin.  Block j handles producer block j's
+// overflow list: it scans the per-bin spill counts (block 0 publishes the
+// first slot of each bin), counts its own records per bin in LDS, reserves one
+// range per touched bin with a single global atomic, and places the record
+// ids through LDS cursors (spilled records clump into few bins: per-record
+// global cursors serialise on them).  Returns at once when nothing spilled
+// (the usual case).
+constexpr int kPlaceThreads = 1024;
+__global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
+  __shared__ uint32_t cur[kScMaxBins], lc[kScMaxBins];
+  __shared__ uint32_t part[kPlaceThreads];
+  const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
+  uint32_t* idx = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec));
+  const OvfBook ob = ovf_book(idx, nrec, k.nbins);
+  if (*ob.cnt == 0u) return;
+  const uint32_t mine = ob.blk[blockIdx.x];
+  if (mine == 0u && blockIdx.x != 0) return;   // block 0 publishes `first`
+  const int per = (k.nbins + kPlaceThreads - 1) / kPlaceThreads, t = threadIdx.x;
+  uint32_t sum = 0;
+  for (int j = 0; j < per; ++j) {
+    const int bb = t * per + j;
+    if (bb < k.nbins) {
+      sum += ob.per_bin[bb];
+      lc[bb] = 0u;
+    }
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < kPlaceThreads; d <<= 1) {   // inclusive scan of the thread sums
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (int j = 0; j < per; ++j) {
+    const int bb = t * per + j;
+    if (bb < k.nbins) {
+      cur[bb] = run;
+      if (blockIdx.x == 0) ob.first[bb] = run;
+      run += ob.per_bin[bb];
+    }
+  }
+  const size_t o0 = (size_t)blockIdx.x * ovf_per_block(k.n_rays);   // this list, relative to the overflow
+  const uint32_t* lst = idx + (size_t)kBwdBlocks * k.nbins * k.cap + o0;
+  auto bin_of = [&](uint32_t s) { return (lst[s] & 0x0fffffffu) >> k.shift; };
+  for (uint32_t s = t; s < mine; s += kPlaceThreads)
+    __hip_atomic_fetch_add(lc + bin_of(s), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  for (int j = 0; j < per; ++j) {
+    const int bb = t * per + j;
+    if (bb < k.nbins && lc[bb])
+      cur[bb] += __hip_atomic_fetch_add(ob.cur + bb, lc[bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (uint32_t s = t; s < mine; s += kPlaceThreads) {
+    const uint32_t pos = __hip_atomic_fetch_add(cur + bin_of(s), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    ob.ids[pos] = (uint32_t)(o0 + s);
+  }
+}
+
 // Records of the bin, flattened over the producers' regions: thread i takes
 // records i, i + 1024, ... (4 at a time, independent loads in flight) and
 // finds each one's region by binary search over the LDS prefix of the
@@ -1987,12 +2226,13 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   const int n4 = (2 << k.shift) / 2;   // f32x4 = 2 accumulators
   for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t b = blockIdx.x;
-  const size_t nrec = bin_records(k.nbins, k.cap);
+  const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
   const f32x4* vals = reinterpret_cast<const f32x4*>(k.bins);
   const uint32_t* idx = reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec);
   const uint32_t* cnt = idx + nrec;
   const float* mxs = reinterpret_cast<const float*>(cnt + (size_t)kBwdBlocks * k.nbins);   // [16][blocks]
-  const uint32_t n_ovf = cnt[(size_t)kBwdBlocks * (k.nbins + 16)];
+  const OvfBook obk = ovf_book(const_cast<uint32_t*>(idx), nrec, k.nbins);
+  const uint32_t n_ovf = *obk.cnt;
   static_assert(kBwdBlocks == 256 && kBinThreads >= 256, "one count per thread of waves 0-3");
   // levels of this bin: one, or all 16 when the whole table is one bin
   const int lev0 = (int)(((uint32_t)b << k.shift) >> k.log2T);
@@ -2076,11 +2316,13 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #endif
       }
   }
-  const uint32_t no = n_ovf < (uint32_t)kOvfRecs ? n_ovf : (uint32_t)kOvfRecs;
-  const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
-  for (uint32_t s = threadIdx.x; s < no; s += kBinThreads) {
-    const uint32_t w = idx[ob + s];
-    if (((w & 0x0fffffffu) >> k.shift) == b) bin_add(acc, se, vals[ob + s], w, sel, tmask, scale);
+  if (n_ovf) {   // this bin's spilled records (bucketed by ovf_place_kernel)
+    const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
+    const uint32_t lo = obk.first[b], hi = lo + obk.per_bin[b];
+    for (uint32_t s = lo + threadIdx.x; s < hi; s += kBinThreads) {
+      const uint32_t o = obk.ids[s];
+      bin_add(acc, se, vals[ob + o], idx[ob + o], sel, tmask, scale);
+    }
   }
   __syncthreads();
   const double inv = 1.0 / (double)scale;
@@ -2149,15 +2391,20 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   g.nbins = 1 << (T + 4 - g.shift);
   const double rpb = (double)((n_rays + kBwdBlocks - 1) / kBwdBlocks);
   const double avg = rpb * (kSf * 4) * ldexp(1.0, g.shift - T);
+  static const int env_cap = [] {   // diagnostic override (HN_BIN_CAP, multiple of 64)
+    const char* e = getenv("HN_BIN_CAP");
+    const int c = e ? atoi(e) : 0;
+    return c > 0 && c % 64 == 0 ? c : 0;
+  }();
+  if (cap_override <= 0) cap_override = env_cap;
   g.cap = cap_override > 0 ? cap_override : (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
-  const size_t nrec = bin_records(g.nbins, g.cap);
-  g.floats = nrec * 5 + (size_t)kBwdBlocks * (g.nbins + 16) + 4;
+  const size_t nrec = bin_records(g.nbins, g.cap, n_rays);
+  g.floats = nrec * 5 + (size_t)kBwdBlocks * (g.nbins + 16) + ovf_book_words(g.nbins, n_rays) + 4;
   return g;
 }
 // Backward schedule: cfg->scatter 1 = float atomics (fused), 2 = binned
 // (split), 0 = binned unless the environment sets HN_SCATTER=atomic.  The
-// binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 21);
-// larger tables take the atomic scatter.
+// binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 22).
 static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   static int env = -1;
   if (env < 0) {
@@ -2166,10 +2413,9 @@ static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   }
   if (!c) return kModeAtomic;
   const int want = c->scatter == 1 ? kModeAtomic : c->scatter == 2 ? kModeSplit : env;
-  if (want != kModeSplit || (16ll << c->grid.log2_hashmap_size) > (long long)kScMaxBins << 13) return kModeAtomic;
-  // the producers address records with 32-bit byte offsets
-  const BinGeom g = bin_geom(c->grid.log2_hashmap_size, n_rays, c->bin_cap);
-  return bin_records(g.nbins, g.cap) * 16 < (1ull << 32) ? kModeSplit : kModeAtomic;
+  (void)n_rays;
+  return want == kModeSplit && (16ll << c->grid.log2_hashmap_size) <= (long long)kScMaxBins << 13 ? kModeSplit
+                                                                                                : kModeAtomic;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
 // coarse-pass feature grads [n][64][32] | d raw [n][256][4] | split: fine
@@ -2358,6 +2604,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (mode != kModeAtomic) {
     BinR r;
     r.bins = k.bins;
+    r.n_rays = a->n_rays;
     r.nbins = bg.nbins;
     r.cap = bg.cap;
     r.shift = bg.shift;
@@ -2366,6 +2613,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.overwrite = a->d_table_mode == 1;
     r.fused = a->table_step != nullptr;
     if (r.fused) r.step = *a->table_step;
+    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
+    if ((st = hip_status(hipGetLastError()))) return st;
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
                        (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
     if ((st = hip_status(hipGetLastError()))) return st;

@@ -139,7 +139,7 @@ typedef struct hn_render_cfg {
   int32_t perturb;        /* 1: stratified jitter from t_rand */
   int32_t scatter;        /* backward table-gradient scatter: 0 auto (binned, unless the
                              environment sets HN_SCATTER=atomic), 1 float atomics,
-                             2 binned (records + exact per-bin owner pass; T <= 21) */
+                             2 binned (records + exact per-bin owner pass; T <= 22) */
   int32_t bin_cap;        /* binned scatter: records per (producer block, bin) region, a
                              multiple of 64; 0 = sized from the batch.  Small values
                              exercise the shared overflow records (tests). */

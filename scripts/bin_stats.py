@@ -13,11 +13,11 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-G_END, W_END, BLOCKS, OVF = 30208, 9344, 256, 1 << 20
+G_END, W_END, BLOCKS = 30208, 9344, 256
 
 
 def bin_geom(T, n):
-    shift = min(14, T + 4)
+    shift = min(13, T + 4)
     nbins = 1 << (T + 4 - shift)
     rpb = (n + BLOCKS - 1) // BLOCKS
     avg = rpb * 192 * 4 * 2.0 ** (shift - T)
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--n-rand", type=int, default=4096)
     ap.add_argument("--log2T", type=int, default=19)
     ap.add_argument("--finest", type=int, default=512)
+    ap.add_argument("--quick", action="store_true", help="counts only (no owner / precision study)")
     a = ap.parse_args()
     import hn_loader
     hn_loader.load()
@@ -56,13 +57,12 @@ def main():
     n, T = a.n_rand, a.log2T
     shift, nbins, cap = bin_geom(T, n)
     off = 2 * G_END + BLOCKS * 2 * W_END + n * 64 * 32 + n * 256 * 4
-    if os.environ.get("HN_SCATTER") == "split":
-        off += n * 192 * 32
-    nrec = BLOCKS * nbins * cap + OVF
+    off += n * 192 * 32                       # fine feature grads (binned schedule)
+    nrec = BLOCKS * nbins * cap + n * 192 * 64   # regions + overflow (ovf_records)
     ws = st.wsb.view(torch.int32)
     idx0 = off + 4 * nrec
     cnt = ws[idx0 + nrec: idx0 + nrec + BLOCKS * nbins].cpu().numpy().astype(np.int64).reshape(nbins, BLOCKS)
-    n_ovf = int(ws[idx0 + nrec + BLOCKS * nbins].item())
+    n_ovf = int(ws[idx0 + nrec + BLOCKS * (nbins + 16)].item())
     tot = int(cnt.sum())
     print(f"B={n} T={T} shift={shift} nbins={nbins} cap={cap} records={tot} ({tot / n:.0f}/ray) "
           f"overflow_count={n_ovf} regions>cap={(cnt > cap).sum()} max={cnt.max()} mean={cnt.mean():.1f}")
@@ -72,6 +72,11 @@ def main():
         print("records per level:", " ".join(str(int(x)) for x in lv))
         mx = cnt.max(1).reshape(-1, bins_per_level).max(1)
         print("max region fill per level:", " ".join(str(int(x)) for x in mx))
+        spill = np.maximum(cnt - cap, 0).sum(1).reshape(-1, bins_per_level).sum(1)
+        print("spilled records per level:", " ".join(str(int(x)) for x in spill))
+    if a.quick:
+        HF.L.check_device_faults()
+        return
     # owner-pass simulation on a few bins: chunks of 1024 flattened records ->
     # 2048 items (entry, owner (e >> 5) & 15); per owner batches of 64 items;
     # the claim rounds a batch needs = max items per tag slot (hashed entry)
