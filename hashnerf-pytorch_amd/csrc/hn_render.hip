@@ -545,8 +545,10 @@ struct WRing {
   f32x4 b[kRing];
 };
 
+// The group's base is formed (and laundered) on the scalar unit, so every load
+// is saddr + lane offset: no per-load 64-bit VALU address arithmetic.
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
-  return *reinterpret_cast<const f32x4*>(opaque_ptr(P) + off + 4 * lane);
+  return *reinterpret_cast<const f32x4*>(opaque_ptr(opaque_ptr(P) + off) + 4 * lane);
 }
 template <int I, int N, typename F>
 HN_DEV void static_for(F&& f) {
@@ -675,16 +677,39 @@ HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval) {
   }
 }
 
+// ReLU (v > 0 ? v : 0, NaN -> 0) with its mask bits.  HN_MASK_INT: integer
+// forms that keep no lane masks live (the compare forms held 16+ SGPR-pair
+// masks across the GEMMs and spilled them to VGPR lanes): relu = max(v, 0)
+// with the sign cleared (-0 -> +0; maxnum drops a NaN), bit = relu > 0 from
+// the relu's bits, and the gradient masked by AND with the sign-extended bit.
+#ifndef HN_MASK_INT
+#define HN_MASK_INT 1
+#endif
 HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
+#if HN_MASK_INT
+    float mx;   // max(v, 0) without maxnum's canonicalising max (MFMA results are never sNaN)
+    asm("v_max_f32 %0, 0, %1" : "=v"(mx) : "v"(v[r]));
+    const uint32_t u = __float_as_uint(mx) & 0x7fffffffu;
+    m |= ((u + 0x7fffffffu) >> 31) << (16 * ob + r);
+    v[r] = __uint_as_float(u);
+#else
     m |= (v[r] > 0.f ? 1u : 0u) << (16 * ob + r);
     v[r] = v[r] > 0.f ? v[r] : 0.f;
+#endif
   }
 }
 HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) g[r] = (m >> (16 * ob + r)) & 1u ? g[r] : 0.f;
+  for (int r = 0; r < 16; ++r) {
+#if HN_MASK_INT
+    const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)m, 16 * ob + r, 1);   // 0 or ~0
+    g[r] = __uint_as_float(__float_as_uint(g[r]) & keep);
+#else
+    g[r] = (m >> (16 * ob + r)) & 1u ? g[r] : 0.f;
+#endif
+  }
 }
 
 // One 32-point tile: recompute the forward (features from the cache), then
