@@ -352,10 +352,8 @@ void render_fwd_kernel(RenderK k) {
 // MFMA accumulators (192 registers, AGPR-resident) for the whole kernel, so a
 // tile's dW costs only its MFMAs -- no per-tile LDS accumulation.  The
 // operands of the dW products (the point index on the MFMA k axis) come from
-// per-wave [row][point] LDS images (row stride kXS = 36 floats: staging
-// ds_write_b32 and the ds_read_b128 operand reads are bank-conflict-free);
-// k-step s of lane half h contracts point 16h + s, so four k-steps are one
-// ds_read_b128 per operand.  ReLU masks are kept as bits.
+// per-wave LDS images of bf16 split parts read back transposed (the weight-
+// gradient operand images below).  ReLU masks are kept as bits.
 //
 // Work units: a coarse unit is one ray's 2 coarse tiles, a fine unit 2 of a
 // ray's 6 fine tiles.  Waves 0-2 run units (wave 0 first every coarse unit of
@@ -363,9 +361,10 @@ void render_fwd_kernel(RenderK k) {
 // tiles' table gradients, handed over through an LDS ring.  The composite
 // backward (d raw per sample) comes from a full-occupancy pre-pass.
 // ---------------------------------------------------------------------------
+// per-wave LDS: the weight-gradient operand images (9 x 4 KiB) in a slab of
+// kRRows x kXS floats (also the fused schedule's slot size unit)
 constexpr int kXS = 36;
-// image rows per wave: features | h0 | [sh16 | geo15] | c0 | c1 | rgb grads
-constexpr int kRF = 0, kRH0 = 32, kRC0in = 96, kRC0 = 128, kRC1 = 192, kRC2 = 256, kRRows = 260;
+constexpr int kRRows = 260;
 constexpr int kB1Waves = 4;
 constexpr int kMW = kB1Waves - 1;                          // MLP waves; wave kMW scatters
 constexpr int kB1Img = kMW * kRRows * kXS;                 // floats (112,320 B)
@@ -408,79 +407,92 @@ struct DW {
   f32x16 c2[2], c1[4], c0[2], s1[2], s0[2];
 };
 
-// image rows [row0, row0 + 32) <- D-layout tile (row row_of(r,h), point p)
-HN_DEV void put_rows(float* X, int row0, const f32x16& v, int lane) {
+// ---- weight-gradient operand images --------------------------------------
+// A 32 x 32 tile of a layer's activations or output grads (rows = features,
+// columns = the tile's points; D layout in registers) is staged as its first
+// two split-f32 parts (hn_common.h: p0 = bf16(x), p1 = bf16(x - p0), the NS = 2
+// split of the dW products) in a per-wave image [32 points][32 features] of
+// bf16 per part (64-B point rows).  The parts come from the split the tile
+// already gets as the B operand of the next GEMM of the chain (gemm_w / _w2
+// with an image sink), so the dW products need no split of their own.
+// dW[o][i] = sum_p G[o][p] X[i][p] contracts the point index (X's column),
+// so both operands are read back transposed by ds_read_b64_tr_b16: lane l
+// gets feature l & 31 of 4 consecutive points per read.  The 8-byte feature
+// quads of point p sit at quad f4 ^ ((p >> 1) & 7): the quad writes of a
+// D-layout tile are 2-way (the minimum for 64 lanes x 8 B on 32 banks), the
+// transposed reads conflict-free.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kImgBlk = 4096;   // bytes per tile image: 2 parts x 2 KiB
+// tile images per wave: features | h0 (2) | [sh16 | sigma | geo15] | c0 (2) |
+// c1 (2) | rgb grads; the grads of the backward reuse c1 (dc1, then ds1) and
+// c0 (dc0, then dh0) once those are consumed
+enum : int { kBF = 0, kBH0 = 1, kBC0in = 3, kBC0 = 4, kBC1 = 6, kBDR = 8, kNImg = 9 };
+static_assert(kNImg * kImgBlk <= kRRows * kXS * 4, "images fit the per-wave LDS");
+
+HN_DEV uint32_t img_off(int blk, int part, int p, int f4) {
+  return (uint32_t)(blk * kImgBlk + part * 2048 + p * 64 + ((f4 ^ ((p >> 1) & 7)) << 3));
+}
+HN_DEV void put_quad(char* Xb, int blk, int part, int p, int f4, uint32_t lo, uint32_t hi) {
+  *reinterpret_cast<uint2*>(Xb + img_off(blk, part, p, f4)) = uint2{lo, hi};
+}
+// Parts 0 and 1 of one split B chunk (elements j = D registers 8c' + j of
+// lane (p, h): rows 16c' + 4h + j for j < 4, 16c' + 8 + 4h + j - 4 after) to
+// quads f4b + h and f4b + 2 + h (f4b = 4c' + the tile's feature offset / 4).
+template <int NS>
+HN_DEV void put_parts(char* Xb, int blk, int f4b, const SP<NS>& s, int lane) {
+  static_assert(NS >= 2, "the images hold two parts");
   const int p = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) X[(row0 + row_of(r, h)) * kXS + p] = v[r];
+  for (int q = 0; q < 2; ++q) {
+    const u32x4 w = __builtin_bit_cast(u32x4, s.p[q]);
+    put_quad(Xb, blk, q, p, f4b + h, w[0], w[1]);
+    put_quad(Xb, blk, q, p, f4b + 2 + h, w[2], w[3]);
+  }
+}
+// A D-layout tile not split by any GEMM of the chain (c1): split and stage it.
+HN_DEV void put_tile(char* Xb, int blk, const f32x16& v, int lane) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) put_parts<2>(Xb, blk, 4 * c, splitn<2>([&](int j) { return v[8 * c + j]; }), lane);
 }
 
-// acc[n][k] += sum over the tile's 32 points of A[arow_n][pt] * B[brow_k][pt];
-// arow / brow are this lane's rows (n = k = lane & 31).
-#ifndef HN_WGRAD_SHARE   // 1: wgrad_n splits each LDS operand row once per chunk
-#define HN_WGRAD_SHARE 1
-#endif
-HN_DEV f32x16 wgrad(const float* X, int arow, int brow, f32x16 acc, int lane) {
-  const int h = lane >> 5;
-  const f32x4* pa = reinterpret_cast<const f32x4*>(X + arow * kXS + 16 * h);
-  const f32x4* pb = reinterpret_cast<const f32x4*>(X + brow * kXS + 16 * h);
-#if HN_SPLIT_W
-  // split-f32 (hn_common.h): K = 16 chunk c, element j of lane half h = point 16h + 8c + j
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const SP<HN_SPLIT_W> a = splitn<HN_SPLIT_W>(pa[2 * c], pa[2 * c + 1]);
-    const SP<HN_SPLIT_W> b = splitn<HN_SPLIT_W>(pb[2 * c], pb[2 * c + 1]);
-    acc = mfma_split<HN_SPLIT_W>(a, b, acc);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  return acc;
-#endif
-  f32x4 an = pa[0], bn = pb[0];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 a = an, b = bn;
-    if (g < 3) {
-      an = pa[g + 1];
-      bn = pb[g + 1];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = mfma(a[j], b[j], acc);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  return acc;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+HN_DEV s16x4 ds_read_tr(const char* a) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(a)));
+}
+// Operand of K = 16 chunk cc (points 16cc .. 16cc + 15) of image tile blk,
+// part q: lane l holds feature l & 31 at points 16cc + 8h + j (element j).
+HN_DEV bf16x8 img_operand(const char* Xb, int blk, int q, int cc, int lane) {
+  const int g = (lane >> 4) & 3, i = lane & 15, h = lane >> 5;
+  const int f4 = 4 * (g & 1) + (i & 3), pt = 16 * cc + 8 * h + (i >> 2);
+  const s16x4 lo = ds_read_tr(Xb + img_off(blk, q, pt, f4));
+  const s16x4 hi = ds_read_tr(Xb + img_off(blk, q, pt + 4, f4));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
-// acc[NB * a + b] += wgrad(X, arow[a], brow[b]): each operand row is read and
-// split once per chunk for all the blocks that use it
+// acc[NB * a + b] += sum over the tile's 32 points of A(ablk[a]) B(bblk[b])^T
+// (two K = 16 chunks, 2-part products in mfma_split's order)
 template <int NA, int NB>
-HN_DEV void wgrad_n(const float* X, const int (&arow)[NA], const int (&brow)[NB], f32x16* acc, int lane) {
-#if HN_SPLIT_W && HN_WGRAD_SHARE
-  const int h = lane >> 5;
+HN_DEV void wgrad_n(const char* Xb, const int (&ablk)[NA], const int (&bblk)[NB], f32x16* acc, int lane) {
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    SP<HN_SPLIT_W> a[NA], b[NB];
+  for (int cc = 0; cc < 2; ++cc) {
+    SP<2> a[NA], b[NB];
 #pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const f32x4* pa = reinterpret_cast<const f32x4*>(X + arow[j] * kXS + 16 * h);
-      a[j] = splitn<HN_SPLIT_W>(pa[2 * c], pa[2 * c + 1]);
-    }
+    for (int j = 0; j < NA; ++j)
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const f32x4* pb = reinterpret_cast<const f32x4*>(X + brow[j] * kXS + 16 * h);
-      b[j] = splitn<HN_SPLIT_W>(pb[2 * c], pb[2 * c + 1]);
-    }
+      for (int q = 0; q < 2; ++q) a[j].p[q] = img_operand(Xb, ablk[j], q, cc, lane);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) b[j].p[q] = img_operand(Xb, bblk[j], q, cc, lane);
 #pragma unroll
     for (int ja = 0; ja < NA; ++ja)
 #pragma unroll
-      for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = mfma_split<HN_SPLIT_W>(a[ja], b[jb], acc[NB * ja + jb]);
+      for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = mfma_split<2>(a[ja], b[jb], acc[NB * ja + jb]);
     __builtin_amdgcn_sched_barrier(0);
   }
-#else
-#pragma unroll
-  for (int ja = 0; ja < NA; ++ja)
-#pragma unroll
-    for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = wgrad(X, arow[ja], brow[jb], acc[NB * ja + jb], lane);
-#endif
 }
 
 // ---- weight-fragment stream ----------------------------------------------
@@ -574,10 +586,13 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
   return a;
 }
 
-// acc += A(segment SEG of the stream) . B, bval(s) = B operand of f32 k-step s
-template <int SEG, typename BF>
-HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
+// acc += A(segment SEG of the stream) . B, bval(s) = B operand of f32 k-step s.
+// IMG >= 0: chunk c's first two B parts also go to image tile IMG + c / 2 at
+// quad offset F4B + 4 (c % 2) (put_parts; Xb = the wave's images).
+template <int SEG, int IMG = -1, int F4B = 0, typename BF>
+HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, char* Xb = nullptr) {
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = reg_ns(R), START = seg_start(SEG);
+  static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
   if constexpr (NS > 0) {                       // split-f32: NS groups per K = 16 chunk
     static_for<0, KS / 8>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
@@ -587,6 +602,7 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
         a.p[q] = as_bf16x8(wring_take<START + NS * c + q>(w, P, lane));
       });
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
+      if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
       acc = mfma_split<NS>(a, b, acc);
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -604,18 +620,13 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval) {
 
 // acc0 / acc1 += blocks 0 / 1 of the paired segment SEG . B: one B split per
 // chunk for both blocks, and two independent accumulator chains
-#ifndef HN_W2_SWP   // 1: software-pipelined B splits (diagnostic A/B)
-#define HN_W2_SWP 0
-#endif
-template <int SEG, typename BF>
-HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int lane, BF bval) {
+template <int SEG, int IMG = -1, int F4B = 0, typename BF>
+HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int lane, BF bval, char* Xb = nullptr) {
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = reg_ns(R), START = seg_start(SEG);
   static_assert(kSegs[SEG].ob < 0, "paired segment");
+  static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
   if constexpr (NS > 0) {
     constexpr int NC = KS / 8;
-#if HN_W2_SWP
-    SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
-#endif
     static_for<0, NC>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
       SP<NS> a0, a1;
@@ -627,22 +638,9 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
         constexpr int q = decltype(qc)::value;
         a1.p[q] = as_bf16x8(wring_take<START + 2 * NS * c + NS + q>(w, P, lane));
       });
-#if HN_W2_SWP
-      // the next chunk's B split (VALU) runs in this chunk's MFMA shadow
-      SP<NS> bn = b;
-      if constexpr (c + 1 < NC) bn = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-      mfma_split2<NS>(a0, a1, b, acc0, acc1);
-      if constexpr (c + 1 < NC) {
-        static_for<0, 2 * (NS == 3 ? 6 : 3)>([&](auto) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // then up to 4 VALU
-        });
-      }
-      b = bn;
-#else
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
+      if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
-#endif
       __builtin_amdgcn_sched_barrier(0);
     });
   } else {
@@ -665,14 +663,14 @@ constexpr int seg_of(int r) {   // first stream segment of region r
     if (kSegs[i].r == r) return i;
   return -1;
 }
-// acc[0..1] += both output blocks of region R . B
-template <int R, typename BF>
-HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval) {
+// acc[0..1] += both output blocks of region R . B (image sink: gemm_w)
+template <int R, int IMG = -1, int F4B = 0, typename BF>
+HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, char* Xb = nullptr) {
   constexpr int S = seg_of(R);
   if constexpr (kSegs[S].ob < 0) {
-    gemm_w2<S>(w, P, acc[0], acc[1], lane, bval);
+    gemm_w2<S, IMG, F4B>(w, P, acc[0], acc[1], lane, bval, Xb);
   } else {
-    acc[0] = gemm_w<S>(w, P, acc[0], lane, bval);
+    acc[0] = gemm_w<S, IMG, F4B>(w, P, acc[0], lane, bval, Xb);
     acc[1] = gemm_w<S + 1>(w, P, acc[1], lane, bval);
   }
 }
@@ -717,97 +715,84 @@ HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
                       const f32x16 c0sh[2], float4 dr, DW& dw) {
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
-  const int p = lane & 31, h = lane >> 5, i = lane & 31;
+  const int h = lane >> 5;
+  char* Xb = reinterpret_cast<char*>(X);
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
-  // ---- forward recompute (models.py:151-174) ----
-  put_rows(X, kRF, feat, lane);
+  // ---- forward recompute (models.py:151-174); each GEMM stages its B
+  // operand's parts as a dW operand image ----
   f32x16 h0[2] = {zero16(), zero16()};
-  gemm2<R_F0>(wr, P, h0, lane, [&](int s) { return feat[s]; });
+  gemm2<R_F0, kBF>(wr, P, h0, lane, [&](int s) { return feat[s]; }, Xb);
   relu_bits(h0[0], mh0, 0);
   relu_bits(h0[1], mh0, 1);
-  put_rows(X, kRH0, h0[0], lane);
-  put_rows(X, kRH0 + 32, h0[1], lane);
-  const f32x16 s1 = gemm_w<seg_of(R_F1)>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; });
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {                 // geo rows 1..15 -> image rows 16..30
-    const int row = row_of(r, h);
-    if (row >= 1) X[(kRC0in + 15 + row) * kXS + p] = s1[r];
-  }
+  const f32x16 s1 = gemm_w<seg_of(R_F1), kBH0>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; }, Xb);
   f32x16 c0[2] = {c0sh[0], c0sh[1]};
-  gemm2<R_F2G>(wr, P, c0, lane, [&](int s) { return s1[s]; });
+  // s1 rows 0..15 = [sigma | geo15] -> features 16..31 of [sh16 | sigma | geo15]
+  gemm2<R_F2G, kBC0in, 4>(wr, P, c0, lane, [&](int s) { return s1[s]; }, Xb);
   relu_bits(c0[0], mc0, 0);
   relu_bits(c0[1], mc0, 1);
-  put_rows(X, kRC0, c0[0], lane);
-  put_rows(X, kRC0 + 32, c0[1], lane);
   {
     f32x16 c1[2] = {zero16(), zero16()};
-    gemm2<R_F3>(wr, P, c1, lane, [&](int s) { return c0[s >> 4][s & 15]; });
+    gemm2<R_F3, kBC0>(wr, P, c1, lane, [&](int s) { return c0[s >> 4][s & 15]; }, Xb);
     relu_bits(c1[0], mc1, 0);
     relu_bits(c1[1], mc1, 1);
-    put_rows(X, kRC1, c1[0], lane);
-    put_rows(X, kRC1 + 32, c1[1], lane);
+    put_tile(Xb, kBC1, c1[0], lane);
+    put_tile(Xb, kBC1 + 1, c1[1], lane);
   }
-  if (h == 0) {
-    X[(kRC2 + 0) * kXS + p] = dr.x;
-    X[(kRC2 + 1) * kXS + p] = dr.y;
-    X[(kRC2 + 2) * kXS + p] = dr.z;
+  if (h == 0) {   // rgb grads: features 0..2 of the kBDR tile (features >= 3 are never stored)
+    const SP<2> d = splitn<2>([&](int j) { return j == 0 ? dr.x : j == 1 ? dr.y : j == 2 ? dr.z : 0.f; });
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const u32x4 w = __builtin_bit_cast(u32x4, d.p[q]);
+      put_quad(Xb, kBDR, q, lane & 31, 0, w[0], w[1]);
+    }
   }
   lds_fence_wave();
-  // ---- color_net.2 ----
-  const int rc2 = kRC2 + (i < 3 ? i : 3);       // rows >= 3 of this block are discarded
+  // ---- color_net.2 (dW rows >= 3 are discarded) ----
   {
-    const int ar[1] = {rc2}, br[2] = {kRC1 + i, kRC1 + 32 + i};
-    wgrad_n<1, 2>(X, ar, br, dw.c2, lane);
+    const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
+    wgrad_n<1, 2>(Xb, ab, bb, dw.c2, lane);
   }
   const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
   f32x16 dc1[2] = {zero16(), zero16()};
   gemm2<R_B4>(wr, P, dc1, lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
   mask_bits(dc1[0], mc1, 0);
   mask_bits(dc1[1], mc1, 1);
-  lds_fence_wave();
-  // ---- color_net.1 (dc1 image over the c1 rows) ----
-  put_rows(X, kRC1, dc1[0], lane);
-  put_rows(X, kRC1 + 32, dc1[1], lane);
-  lds_fence_wave();
-  {
-    const int ar[2] = {kRC1 + i, kRC1 + 32 + i}, br[2] = {kRC0 + i, kRC0 + 32 + i};
-    wgrad_n<2, 2>(X, ar, br, dw.c1, lane);     // dw.c1[2 * nb + kb]
-  }
+  // ---- color_net.1 (dc1 image over c1) ----
   f32x16 dc0[2] = {zero16(), zero16()};
-  gemm2<R_B3>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; });
+  gemm2<R_B3, kBC1>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; }, Xb);
   mask_bits(dc0[0], mc0, 0);
   mask_bits(dc0[1], mc0, 1);
   lds_fence_wave();
-  // ---- color_net.0: X = [sh16 | geo15] (dc0 image over the c0 rows) ----
-  put_rows(X, kRC0, dc0[0], lane);
-  put_rows(X, kRC0 + 32, dc0[1], lane);
-  lds_fence_wave();
   {
-    const int ar[2] = {kRC0 + i, kRC0 + 32 + i}, br[1] = {kRC0in + i};
-    wgrad_n<2, 1>(X, ar, br, dw.c0, lane);
+    const int ab[2] = {kBC1, kBC1 + 1}, bb[2] = {kBC0, kBC0 + 1};
+    wgrad_n<2, 2>(Xb, ab, bb, dw.c1, lane);     // dw.c1[2 * nb + kb]
   }
-  f32x16 ds1 = gemm_w<seg_of(R_B2G)>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; });
+  // ---- color_net.0 (dc0 image over c0; B = [sh16 | sigma | geo15]) ----
+  f32x16 ds1 = gemm_w<seg_of(R_B2G), kBC0>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; }, Xb);
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
-  // ---- sigma_net.1 (ds1 image over the c1 rows; rows 16..31 are zero) ----
-  put_rows(X, kRC1, ds1, lane);
   lds_fence_wave();
   {
-    const int ar[1] = {kRC1 + i}, br[2] = {kRH0 + i, kRH0 + 32 + i};
-    wgrad_n<1, 2>(X, ar, br, dw.s1, lane);
+    const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBC0in};
+    wgrad_n<2, 1>(Xb, ab, bb, dw.c0, lane);
   }
+  // ---- sigma_net.1 (ds1 image over dc1's first tile; rows 16..31 discarded) ----
   f32x16 dh0[2] = {zero16(), zero16()};
-  gemm2<R_B1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; });
+  gemm2<R_B1, kBC1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; }, Xb);
   mask_bits(dh0[0], mh0, 0);
   mask_bits(dh0[1], mh0, 1);
-  // ---- sigma_net.0 (dh0 image over the c0 rows) ----
-  put_rows(X, kRC0, dh0[0], lane);
-  put_rows(X, kRC0 + 32, dh0[1], lane);
   lds_fence_wave();
   {
-    const int ar[2] = {kRC0 + i, kRC0 + 32 + i}, br[1] = {kRF + i};
-    wgrad_n<2, 1>(X, ar, br, dw.s0, lane);
+    const int ab[1] = {kBC1}, bb[2] = {kBH0, kBH0 + 1};
+    wgrad_n<1, 2>(Xb, ab, bb, dw.s1, lane);
   }
-  const f32x16 dfeat = gemm_w<seg_of(R_B0)>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; });
+  // ---- sigma_net.0 (dh0 image over dc0) ----
+  const f32x16 dfeat =
+      gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; }, Xb);
+  lds_fence_wave();
+  {
+    const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBF};
+    wgrad_n<2, 1>(Xb, ab, bb, dw.s0, lane);
+  }
   static_for<kTileGroups, kTilePeriod - kTileGroups>([&](auto gc) {   // pad groups: keep the ring
     (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
   });
@@ -1792,8 +1777,15 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(drs + 128 * t);
   float sh8[8], shx8[8];
   ray_sh(r, h, sh8, shx8);
+  {   // sh part of color_net.0's input: features 8h .. 8h + 7 of the [sh16 | sigma | geo15] image
+    const SP<2> sp = splitn<2>([&](int j) { return shx8[j]; });
 #pragma unroll
-  for (int j = 0; j < 8; ++j) X[(kRC0in + 8 * h + j) * kXS + p] = shx8[j];
+    for (int q = 0; q < 2; ++q) {
+      const u32x4 w = __builtin_bit_cast(u32x4, sp.p[q]);
+      put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h, w[0], w[1]);
+      put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h + 1, w[2], w[3]);
+    }
+  }
   const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
   // color_net.0 applied to the sh part: the same for every point of the ray
   // (and bit-identical to starting each point's chain with it)
@@ -1938,6 +1930,24 @@ HN_DEV void dw_block(float* acc, int base, int ld, int n0, int nmax, int k0, int
   }
 }
 
+// color_net.0's dW block: its columns are the image features [sh16 | sigma |
+// geo15] (b1_tile): feature 16 (sigma, no weight) is dropped, 17..31 are
+// weight columns 16..30.
+template <bool STORE>
+HN_DEV void dw_block_c0(float* acc, int nb, const f32x16& d, int lane) {
+  const int i = lane & 31, h = lane >> 5;
+  if (i == 16) return;
+  const int col = i < 16 ? i : i - 1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float* dst = acc + W_C0 + (32 * nb + row_of(r, h)) * 31 + col;
+    if constexpr (STORE)
+      *dst = d[r];
+    else
+      atomicAdd(dst, d[r]);
+  }
+}
+
 template <bool STORE>
 HN_DEV void dw_flush(const DW& dw, float* acc, int lane) {
 #pragma unroll
@@ -1948,7 +1958,7 @@ HN_DEV void dw_flush(const DW& dw, float* acc, int lane) {
     for (int kb = 0; kb < 2; ++kb)
       dw_block<STORE>(acc, W_C1, 64, 32 * nb, 64, 32 * kb, 64, dw.c1[2 * nb + kb], lane);
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) dw_block<STORE>(acc, W_C0, 31, 32 * nb, 64, 0, 31, dw.c0[nb], lane);
+  for (int nb = 0; nb < 2; ++nb) dw_block_c0<STORE>(acc, nb, dw.c0[nb], lane);
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) dw_block<STORE>(acc, W_S1, 64, 0, 16, 32 * kb, 64, dw.s1[kb], lane);
 #pragma unroll
