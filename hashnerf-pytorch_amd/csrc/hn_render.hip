@@ -557,10 +557,24 @@ struct WRing {
   f32x4 b[kRing];
 };
 
-// The group's base is formed (and laundered) on the scalar unit, so every load
-// is saddr + lane offset: no per-load 64-bit VALU address arithmetic.
+// A raw buffer load: descriptor over the packed weights, voffset = the lane's
+// 16 bytes, soffset = the group's byte offset laundered on the scalar unit
+// (not hoisted: ~100 loop-invariant offsets would spill SGPRs), so a load
+// costs no vector address arithmetic (a global load of base + group + lane
+// took a 64-bit VALU add per load).
+#ifndef HN_WBUF
+#define HN_WBUF 1
+#endif
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
+#if HN_WBUF
+  int so = off * 4;
+  asm volatile("" : "+s"(so));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(opaque_ptr(P)), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+#else
   return *reinterpret_cast<const f32x4*>(opaque_ptr(opaque_ptr(P) + off) + 4 * lane);
+#endif
 }
 template <int I, int N, typename F>
 HN_DEV void static_for(F&& f) {
