@@ -86,6 +86,44 @@ HN_DEV void voxel_level(const float x[3], const float xc[3], const float gs[3],
   v.h[7] = (x1 ^ y1 ^ z1) & mask;
 }
 
+// The cell's quotient q = (xc - min) / g from the correctly rounded reciprocal
+// rg = RN(1/g): q0 = num * rg, r = fma(-g, q0, num) (exact), q = fma(r, rg, q0)
+// is the correctly rounded quotient for num >= 2^-100 (one correction step with
+// RN(1/g); checked against IEEE division on 575 M quotients over the grid
+// sizes of six boxes x three finest resolutions, scripts/div_check.c), and
+// below that both floors are 0.  Only the floor is used: 3 instructions for
+// the division's ~11.
+HN_DEV int32_t cell_floor(float num, float g, float rg) {
+  const float q0 = num * rg;
+  const float r = __builtin_fmaf(-g, q0, num);
+  return (int32_t)floorf(__builtin_fmaf(r, rg, q0));
+}
+// voxel_level with the cells from cell_floor (rg[a] = RN(1/gs[a])); the
+// weights keep the reference's IEEE divisions.
+HN_DEV void voxel_level_rcp(const float x[3], const float xc[3], const float gs[3], const float rg[3],
+                            const float bmin[3], uint32_t mask, Voxel& v) {
+  uint32_t c[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int32_t i = cell_floor(xc[a] - bmin[a], gs[a], rg[a]);   // floor((x - min) / g).int()
+    const float vmin = (float)i * gs[a] + bmin[a];
+    const float vmax = vmin + gs[a];
+    v.w[a] = (x[a] - vmin) / (vmax - vmin);
+    c[a] = (uint32_t)i;
+  }
+  const uint32_t x0 = c[0], x1 = c[0] + 1u;
+  const uint32_t y0 = c[1] * kPrimeY, y1 = (c[1] + 1u) * kPrimeY;
+  const uint32_t z0 = c[2] * kPrimeZ, z1 = (c[2] + 1u) * kPrimeZ;
+  v.h[0] = (x0 ^ y0 ^ z0) & mask;
+  v.h[1] = (x0 ^ y0 ^ z1) & mask;
+  v.h[2] = (x0 ^ y1 ^ z0) & mask;
+  v.h[3] = (x0 ^ y1 ^ z1) & mask;
+  v.h[4] = (x1 ^ y0 ^ z0) & mask;
+  v.h[5] = (x1 ^ y0 ^ z1) & mask;
+  v.h[6] = (x1 ^ y1 ^ z0) & mask;
+  v.h[7] = (x1 ^ y1 ^ z1) & mask;
+}
+
 // voxel_level that also returns the integer cell (run detection along rays).
 HN_DEV void voxel_level_cell(const float x[3], const float xc[3], const float gs[3],
                              const float bmin[3], uint32_t mask, Voxel& v, uint32_t cell[3]) {

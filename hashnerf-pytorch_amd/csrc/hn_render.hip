@@ -129,6 +129,12 @@ HN_DEV void load_feat(const float* __restrict__ base, int64_t ray, int tile, int
   }
 }
 
+// grid sizes [16][3] staged in LDS (saves 48 SGPRs), then their reciprocals
+constexpr int kGsRcp = 48, kGsLds = 96;
+
+#ifndef HN_CELL_RCP   // 1: cells from cell_floor (hn_common.h) in the forward's encode
+#define HN_CELL_RCP 1
+#endif
 // Hash-encode one point into the 32-feature tile layout (lane half h owns
 // levels tile_level(m, h), m = 0..7).  hash_encoding.py:84-110.
 HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __restrict__ table, const float pt[3], int h,
@@ -142,8 +148,13 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     const int l0 = tile_level(m, 0), l1 = tile_level(m, 1);
     const uint32_t l = h ? l1 : l0;
     const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
+    const float rg[3] = {gsl[kGsRcp + 3 * l], gsl[kGsRcp + 3 * l + 1], gsl[kGsRcp + 3 * l + 2]};
     Voxel v;
+#if HN_CELL_RCP
+    voxel_level_rcp(pt, xc, gs, rg, g.bmin, mask, v);
+#else
     voxel_level(pt, xc, gs, g.bmin, mask, v);
+#endif
     float f0, f1;
     encode_level_off(table, l << g.log2T, v, f0, f1);
     feat[2 * m] = f0;
@@ -162,8 +173,6 @@ HN_DEV void ray_sh(const Ray& r, int h, float sh8[8], float shx8[8]) {
   }
 }
 
-// grid sizes [16][3] staged in LDS (saves 48 SGPRs), then their reciprocals
-constexpr int kGsRcp = 48, kGsLds = 96;
 
 HN_DEV void stage_grid_sizes(const GridArgs& g, float* gsl) {
   if (threadIdx.x < 48) {
@@ -689,11 +698,13 @@ HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, ch
   }
 }
 
-// ReLU (v > 0 ? v : 0, NaN -> 0) with its mask bits.  HN_MASK_INT: integer
-// forms that keep no lane masks live (the compare forms held 16+ SGPR-pair
-// masks across the GEMMs and spilled them to VGPR lanes): relu = max(v, 0)
-// with the sign cleared (-0 -> +0; maxnum drops a NaN), bit = relu > 0 from
+// ReLU with its mask bits.  HN_MASK_INT: integer forms that keep no lane masks
+// live (the compare forms held 16+ SGPR-pair masks across the GEMMs and
+// spilled them to VGPR lanes): relu = the bits with the sign-extended sign
+// cleared (v > 0 ? v : 0 for every non-NaN v, -0 -> +0), bit = relu > 0 from
 // the relu's bits, and the gradient masked by AND with the sign-extended bit.
+// (No inline asm here: an asm operand that is an MFMA result gets none of the
+// MFMA-to-VALU wait states the compiler inserts for its own instructions.)
 #ifndef HN_MASK_INT
 #define HN_MASK_INT 1
 #endif
@@ -701,9 +712,8 @@ HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
 #if HN_MASK_INT
-    float mx;   // max(v, 0) without maxnum's canonicalising max (MFMA results are never sNaN)
-    asm("v_max_f32 %0, 0, %1" : "=v"(mx) : "v"(v[r]));
-    const uint32_t u = __float_as_uint(mx) & 0x7fffffffu;
+    const uint32_t b = __float_as_uint(v[r]);
+    const uint32_t u = b & ~(uint32_t)((int32_t)b >> 31);
     m |= ((u + 0x7fffffffu) >> 31) << (16 * ob + r);
     v[r] = __uint_as_float(u);
 #else
@@ -1396,20 +1406,14 @@ HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
   }
 }
 
-// Voxel of one (point, level) for the split scatter: the cell is the IEEE
-// quotient's floor (the forward's), taken from num * RN(1/g) when that product
-// is farther than its error bound (1.5 ulp, doubled) from an integer, else
-// from the division itself; the weights are the reference's IEEE divisions.
+// Voxel of one (point, level) for the split scatter: the cell from cell_floor
+// (the forward's), the weights by the reference's IEEE divisions.
 HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], const float xc[3], int l,
                         int32_t cell[3], float w[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const float gs = gsl[3 * l + a];
-    const float num = xc[a] - g.bmin[a];
-    float q = num * gsl[kGsRcp + 3 * l + a];
-    const float fq = floorf(q), fr = q - fq;
-    const float tol = fmaxf(q, 1.f) * 0x1p-21f;
-    const int32_t i = (fr < tol || fr > 1.f - tol) ? (int32_t)floorf(num / gs) : (int32_t)fq;
+    const int32_t i = cell_floor(xc[a] - g.bmin[a], gs, gsl[kGsRcp + 3 * l + a]);
     const float vmin = (float)i * gs + g.bmin[a];
     const float vmax = vmin + gs;
     w[a] = (pt[a] - vmin) / (vmax - vmin);
