@@ -432,6 +432,20 @@ HN_DEV T* opaque_ptr(T* p) {
   return (T*)((__attribute__((address_space(1))) T*)v);
 }
 
+// One 1-KiB packed weight-fragment group (lane's 16 bytes at float offset off
+// of P): a raw buffer load, voffset = the lane's 16 bytes, soffset = the
+// group's byte offset laundered on the scalar unit (not hoisted: ~100
+// loop-invariant offsets would spill SGPRs), so a load costs no vector
+// address arithmetic (a global load of base + group + lane took a 64-bit
+// VALU add per load).
+HN_DEV f32x4 frag_load(const float* P, int off, int lane) {
+  int so = off * 4;
+  asm volatile("" : "+s"(so));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(opaque_ptr(P)), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+}
+
 // ---------------------------------------------------------------------------
 // Keyed 4-round Feistel permutation of [0, 2^(2 half)) (pixel sampling without
 // replacement, hn_train.hip; ray scrambling in the render backward) and its

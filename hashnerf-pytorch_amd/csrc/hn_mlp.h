@@ -79,21 +79,30 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 #ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk
 #define HN_GEMM_PF 1
 #endif
+#ifndef HN_FRAG_BUF  // 1: fragment groups through frag_load (buffer loads, scalar offsets)
+#define HN_FRAG_BUF 1
+#endif
 #ifndef HN_GEMM_SWP  // 1: the next chunk's B split is interleaved with this chunk's MFMAs
 #define HN_GEMM_SWP 0
 #endif
 template <int R, typename BF>
 HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF bval) {
   constexpr int KS = kRegKS[R], NS = reg_ns(R), GPO = reg_gpo(R), OFF = reg_off(R);
+#if HN_FRAG_BUF
+  // fragment group g of this block: frag_load (scalar offsets, hn_common.h)
+  auto ld = [&](int g) { return frag_load(P, OFF + (ob * GPO + g) * 256, lane); };
+#else
   // opaque BEFORE the offset: keeps hipcc from precomputing ~50 uniform GEMM
   // base addresses at the top of the tile loop (SGPR pairs that then spill)
   const float* base = opaque_ptr(P) + OFF + ob * GPO * 256 + lane * 4;
+  auto ld = [&](int g) { return *reinterpret_cast<const f32x4*>(base + g * 256); };
+#endif
   if constexpr (NS > 0 && !HN_GEMM_PF) {        // split-f32, fragments loaded at use
 #pragma unroll
     for (int c = 0; c < KS / 8; ++c) {
       SP<NS> a;
 #pragma unroll
-      for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + (NS * c + q) * 256));
+      for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(ld(NS * c + q));
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
       acc = mfma_split<NS>(a, b, acc);
       __builtin_amdgcn_sched_barrier(0);
@@ -102,7 +111,7 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
   } else if constexpr (NS > 0) {                // split-f32 on the bf16 MFMA
     SP<NS> an;
 #pragma unroll
-    for (int q = 0; q < NS; ++q) an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + q * 256));
+    for (int q = 0; q < NS; ++q) an.p[q] = as_bf16x8(ld(q));
 #if HN_GEMM_SWP
     SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
 #endif
@@ -112,7 +121,7 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
       if (c + 1 < KS / 8) {
 #pragma unroll
         for (int q = 0; q < NS; ++q)
-          an.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(base + (NS * (c + 1) + q) * 256));
+          an.p[q] = as_bf16x8(ld(NS * (c + 1) + q));
       }
 #if HN_GEMM_SWP
       // the next chunk's split (VALU) goes into this chunk's MFMA gaps
@@ -135,11 +144,11 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
     }
     return acc;
   } else {
-    f32x4 an = *reinterpret_cast<const f32x4*>(base);
+    f32x4 an = ld(0);
 #pragma unroll
     for (int g = 0; g < KS / 4; ++g) {
       const f32x4 a = an;
-      if (g + 1 < KS / 4) an = *reinterpret_cast<const f32x4*>(base + (g + 1) * 256);
+      if (g + 1 < KS / 4) an = ld(g + 1);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
       __builtin_amdgcn_sched_barrier(0);

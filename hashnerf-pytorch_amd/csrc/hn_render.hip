@@ -566,21 +566,14 @@ struct WRing {
   f32x4 b[kRing];
 };
 
-// A raw buffer load: descriptor over the packed weights, voffset = the lane's
-// 16 bytes, soffset = the group's byte offset laundered on the scalar unit
-// (not hoisted: ~100 loop-invariant offsets would spill SGPRs), so a load
-// costs no vector address arithmetic (a global load of base + group + lane
-// took a 64-bit VALU add per load).
+// Weight-fragment group load: frag_load (hn_common.h, raw buffer load with a
+// scalar offset); HN_WBUF 0 = the former global load of base + group + lane.
 #ifndef HN_WBUF
 #define HN_WBUF 1
 #endif
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
 #if HN_WBUF
-  int so = off * 4;
-  asm volatile("" : "+s"(so));
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(opaque_ptr(P)), (short)0, 0x7fffffff, 0x00020000);
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+  return frag_load(P, off, lane);
 #else
   return *reinterpret_cast<const f32x4*>(opaque_ptr(opaque_ptr(P) + off) + 4 * lane);
 #endif
@@ -2178,6 +2171,8 @@ struct BinR {
   hn_radam_tensor step;
 };
 constexpr int kBinThreads = 1024;
+constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2^13 floats / 4 / 1024)
+static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
 #ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
 #define HN_BR_DIAG 0
 #endif
@@ -2277,8 +2272,25 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __shared__ uint32_t wsum[kBwdBlocks / 64], wmax[kBwdBlocks / 64];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(acc4);
   const int n4 = (2 << k.shift) / 2;   // f32x4 = 2 accumulators
-  for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t b = blockIdx.x;
+  const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
+  const int nd4 = (2 << k.shift) / 4;             // float4s of the slice (<= 4 per thread)
+  // the fused step's optimizer state of this thread's slice entries, loaded
+  // before the records: its latency hides under the record phase instead of
+  // opening the epilogue
+  float4 sp[kSliceF4], sm[kSliceF4], sv[kSliceF4];
+  if (k.fused) {
+#pragma unroll
+    for (int j = 0; j < kSliceF4; ++j) {
+      const int i = threadIdx.x + j * kBinThreads;
+      if (i < nd4) {
+        sp[j] = reinterpret_cast<const float4*>(k.step.p + e0)[i];
+        sm[j] = reinterpret_cast<const float4*>(k.step.m + e0)[i];
+        sv[j] = reinterpret_cast<const float4*>(k.step.v + e0)[i];
+      }
+    }
+  }
+  for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
   const f32x4* vals = reinterpret_cast<const f32x4*>(k.bins);
   const uint32_t* idx = reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec);
@@ -2379,10 +2391,11 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   }
   __syncthreads();
   const double inv = 1.0 / (double)scale;
-  const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
   float4* dst = k.d_table ? reinterpret_cast<float4*>(k.d_table + e0) : nullptr;
-  const int nd4 = (2 << k.shift) / 4;
-  for (int i = threadIdx.x; i < nd4; i += kBinThreads) {   // entries 2i, 2i + 1
+#pragma unroll
+  for (int j = 0; j < kSliceF4; ++j) {   // entries 2i, 2i + 1
+    const int i = threadIdx.x + j * kBinThreads;
+    if (i >= nd4) break;
     float4 a;
     a.x = (float)((double)(long long)acc[2 * i] * inv);
     a.y = (float)((double)(long long)acc[se + 2 * i] * inv);
@@ -2396,17 +2409,14 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       dst[i] = a;
     }
     if (k.fused) {   // RAdam on these 4 table elements (radam_kernel's update, same op forms)
-      float4* pp = reinterpret_cast<float4*>(k.step.p + e0) + i;
-      float4* mp = reinterpret_cast<float4*>(k.step.m + e0) + i;
-      float4* vp = reinterpret_cast<float4*>(k.step.v + e0) + i;
-      float4 p = *pp, m = *mp, v = *vp;
+      float4 p = sp[j], m = sm[j], v = sv[j];
       radam_elem(k.step, p.x, a.x, m.x, v.x);
       radam_elem(k.step, p.y, a.y, m.y, v.y);
       radam_elem(k.step, p.z, a.z, m.z, v.z);
       radam_elem(k.step, p.w, a.w, m.w, v.w);
-      *mp = m;
-      *vp = v;
-      if (k.step.mode != 0) *pp = p;
+      reinterpret_cast<float4*>(k.step.m + e0)[i] = m;
+      reinterpret_cast<float4*>(k.step.v + e0)[i] = v;
+      if (k.step.mode != 0) reinterpret_cast<float4*>(k.step.p + e0)[i] = p;
     }
   }
 }
