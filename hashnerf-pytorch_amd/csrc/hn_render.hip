@@ -2172,6 +2172,9 @@ struct BinR {
 };
 constexpr int kBinThreads = 1024;
 constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2^13 floats / 4 / 1024)
+#ifndef HN_BR_PF   // fused step's state loads: 0 in the epilogue, 1 at kernel start, 2 after the setup, 3 after the last record fetch
+#define HN_BR_PF 1
+#endif
 static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
 #ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
 #define HN_BR_DIAG 0
@@ -2266,7 +2269,20 @@ __global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
 // records i, i + 1024, ... (4 at a time, independent loads in flight) and
 // finds each one's region by binary search over the LDS prefix of the
 // regions' counts.
+#ifndef HN_BR_PROF   // diagnostic: phase timers of the owner pass (scripts/br_profile.sh)
+#define HN_BR_PROF 0
+#endif
+#if HN_BR_PROF
+__device__ unsigned long long g_brprof[8];
+#define HN_BR_T(i) do { __syncthreads(); if (threadIdx.x == 0) { const uint64_t n_ = __builtin_amdgcn_s_memtime(); \
+    atomicAdd(&g_brprof[i], (unsigned long long)(n_ - t_br)); t_br = n_; } } while (0)
+#else
+#define HN_BR_T(i) ((void)0)
+#endif
 __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
+#if HN_BR_PROF
+  uint64_t t_br = __builtin_amdgcn_s_memtime();
+#endif
   extern __shared__ f32x4 acc4[];
   __shared__ uint32_t pre[kBwdBlocks + 1];
   __shared__ uint32_t wsum[kBwdBlocks / 64], wmax[kBwdBlocks / 64];
@@ -2275,11 +2291,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   const uint32_t b = blockIdx.x;
   const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
   const int nd4 = (2 << k.shift) / 4;             // float4s of the slice (<= 4 per thread)
-  // the fused step's optimizer state of this thread's slice entries, loaded
-  // before the records: its latency hides under the record phase instead of
-  // opening the epilogue
   float4 sp[kSliceF4], sm[kSliceF4], sv[kSliceF4];
-  if (k.fused) {
+  auto load_state = [&]() {
 #pragma unroll
     for (int j = 0; j < kSliceF4; ++j) {
       const int i = threadIdx.x + j * kBinThreads;
@@ -2289,7 +2302,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
         sv[j] = reinterpret_cast<const float4*>(k.step.v + e0)[i];
       }
     }
-  }
+  };
+  if (HN_BR_PF == 1 && k.fused) load_state();
   for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
   const f32x4* vals = reinterpret_cast<const f32x4*>(k.bins);
@@ -2333,6 +2347,19 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __syncthreads();
   const uint32_t total = pre[kBwdBlocks];
   const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u, se = 1u << k.shift;
+  HN_BR_T(0);   // accumulator zeroing, counts, prefix, scale
+  if (HN_BR_PF == 2 && k.fused) load_state();
+  // HN_BR_PF 3: the fused step's optimizer state loaded right after the
+  // thread's last record fetch (vmcnt waits are in order: loaded earlier it is
+  // waited for with the first records, later its latency opens the epilogue)
+  bool pf_done = !k.fused || HN_BR_PF != 3;
+  auto prefetch_state = [&]() {
+    load_state();
+    pf_done = true;
+  };
+  auto after_fetch = [&](uint32_t next_fetch) {   // no fetch at next_fetch or later
+    if (!pf_done && next_fetch >= total) prefetch_state();
+  };
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
   // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found by
   // a binary search over the regions' prefix (measured faster than one search
@@ -2356,10 +2383,16 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   f32x4 va[4], vb[4];
   uint32_t wa[4], wb[4];
   uint32_t r0 = threadIdx.x;
-  if (r0 < total) fetch(r0, va, wa);
+  if (r0 < total) {
+    fetch(r0, va, wa);
+    after_fetch(r0 + 4 * kBinThreads);
+  }
   for (; r0 < total; r0 += 8 * kBinThreads) {
     const uint32_t r1 = r0 + 4 * kBinThreads;
-    if (r1 < total) fetch(r1, vb, wb);
+    if (r1 < total) {
+      fetch(r1, vb, wb);
+      after_fetch(r1 + 4 * kBinThreads);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (r0 + q * kBinThreads < total) {
@@ -2370,7 +2403,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #endif
       }
     if (r1 >= total) break;
-    if (r1 + 4 * kBinThreads < total) fetch(r1 + 4 * kBinThreads, va, wa);
+    if (r1 + 4 * kBinThreads < total) {
+      fetch(r1 + 4 * kBinThreads, va, wa);
+      after_fetch(r1 + 8 * kBinThreads);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (r1 + q * kBinThreads < total) {
@@ -2381,6 +2417,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #endif
       }
   }
+  if (!pf_done) prefetch_state();   // threads without records
+  HN_BR_T(1);   // region records
   if (n_ovf) {   // this bin's spilled records (bucketed by ovf_place_kernel)
     const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
     const uint32_t lo = obk.first[b], hi = lo + obk.per_bin[b];
@@ -2390,6 +2428,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     }
   }
   __syncthreads();
+  HN_BR_T(2);   // overflow records
   const double inv = 1.0 / (double)scale;
   float4* dst = k.d_table ? reinterpret_cast<float4*>(k.d_table + e0) : nullptr;
 #pragma unroll
@@ -2409,6 +2448,11 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       dst[i] = a;
     }
     if (k.fused) {   // RAdam on these 4 table elements (radam_kernel's update, same op forms)
+      if (HN_BR_PF == 0) {
+        sp[j] = reinterpret_cast<const float4*>(k.step.p + e0)[i];
+        sm[j] = reinterpret_cast<const float4*>(k.step.m + e0)[i];
+        sv[j] = reinterpret_cast<const float4*>(k.step.v + e0)[i];
+      }
       float4 p = sp[j], m = sm[j], v = sv[j];
       radam_elem(k.step, p.x, a.x, m.x, v.x);
       radam_elem(k.step, p.y, a.y, m.y, v.y);
@@ -2419,6 +2463,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       if (k.step.mode != 0) reinterpret_cast<float4*>(k.step.p + e0)[i] = p;
     }
   }
+  HN_BR_T(3);   // conversion, RAdam, stores issued
 }
 
 static int32_t check_cfg(const hn_render_cfg* c) {
@@ -2687,9 +2732,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
       (void)hipStreamSynchronize(s);
       (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_brprof), sizeof(f));
       const double nb = (double)bg.nbins;
-      fprintf(stderr, "hn_br_profile per bin (wave 0): top+count %.0f B1 %.0f prefix+B2 %.0f stage+B3 %.0f apply %.0f"
-              " | rounds %.1f batches %.1f per bin\n", f[0] / nb, f[1] / nb, f[2] / nb, f[3] / nb, f[4] / nb,
-              f[5] / nb, f[6] / nb);
+      fprintf(stderr, "hn_br_profile cycles per bin: setup %.0f records %.0f overflow %.0f epilogue %.0f\n",
+              f[0] / nb, f[1] / nb, f[2] / nb, f[3] / nb);
       memset(f, 0, sizeof(f));
       (void)hipMemcpyToSymbol(HIP_SYMBOL(g_brprof), f, sizeof(f));
     }
