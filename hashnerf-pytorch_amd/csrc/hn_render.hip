@@ -2101,7 +2101,7 @@ void render_bwd_kernel(B1K k) {
 // deterministic.
 constexpr int kSlabGroups = 16;
 __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs,
-                                                                       hn_mlp_grad dc, hn_mlp_grad df) {
+                                                                       hn_mlp_grad dc, hn_mlp_grad df, int overwrite) {
   __shared__ float part[kSlabGroups][64];
   const int lane = threadIdx.x & 63;
   const int e = blockIdx.x * 64 + lane;
@@ -2136,7 +2136,7 @@ __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const flo
   else if (i < W_C1) dst = d.color0 + (i - W_C0);
   else if (i < W_C2) dst = d.color1 + (i - W_C1);
   else dst = d.color2 + (i - W_C2);
-  *dst += s;
+  *dst = overwrite ? s : *dst + s;
 }
 
 // Owner pass of the binned scatter: workgroup b sums every record of bin b
@@ -2172,8 +2172,13 @@ struct BinR {
 };
 constexpr int kBinThreads = 1024;
 constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2^13 floats / 4 / 1024)
-#ifndef HN_BR_PF   // fused step's state loads: 0 in the epilogue, 1 at kernel start, 2 after the setup, 3 after the last record fetch
-#define HN_BR_PF 1
+// The fused step's optimizer-state loads: 0 in the epilogue; 1 at kernel
+// start.  Measured on one box (config 2): 207.5 vs 214.8 / 204.5 us; loaded
+// after the setup 238 us, after the thread's last record fetch 217 us (64
+// VGPR spills): vmcnt waits are in order, so an earlier issue only moves the
+// wait to the first records.
+#ifndef HN_BR_PF
+#define HN_BR_PF 0
 #endif
 static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
 #ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
@@ -2348,18 +2353,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   const uint32_t total = pre[kBwdBlocks];
   const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u, se = 1u << k.shift;
   HN_BR_T(0);   // accumulator zeroing, counts, prefix, scale
-  if (HN_BR_PF == 2 && k.fused) load_state();
-  // HN_BR_PF 3: the fused step's optimizer state loaded right after the
-  // thread's last record fetch (vmcnt waits are in order: loaded earlier it is
-  // waited for with the first records, later its latency opens the epilogue)
-  bool pf_done = !k.fused || HN_BR_PF != 3;
-  auto prefetch_state = [&]() {
-    load_state();
-    pf_done = true;
-  };
-  auto after_fetch = [&](uint32_t next_fetch) {   // no fetch at next_fetch or later
-    if (!pf_done && next_fetch >= total) prefetch_state();
-  };
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
   // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found by
   // a binary search over the regions' prefix (measured faster than one search
@@ -2383,16 +2376,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   f32x4 va[4], vb[4];
   uint32_t wa[4], wb[4];
   uint32_t r0 = threadIdx.x;
-  if (r0 < total) {
-    fetch(r0, va, wa);
-    after_fetch(r0 + 4 * kBinThreads);
-  }
+  if (r0 < total) fetch(r0, va, wa);
   for (; r0 < total; r0 += 8 * kBinThreads) {
     const uint32_t r1 = r0 + 4 * kBinThreads;
-    if (r1 < total) {
-      fetch(r1, vb, wb);
-      after_fetch(r1 + 4 * kBinThreads);
-    }
+    if (r1 < total) fetch(r1, vb, wb);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (r0 + q * kBinThreads < total) {
@@ -2403,10 +2390,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #endif
       }
     if (r1 >= total) break;
-    if (r1 + 4 * kBinThreads < total) {
-      fetch(r1 + 4 * kBinThreads, va, wa);
-      after_fetch(r1 + 8 * kBinThreads);
-    }
+    if (r1 + 4 * kBinThreads < total) fetch(r1 + 4 * kBinThreads, va, wa);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (r1 + q * kBinThreads < total) {
@@ -2417,7 +2401,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #endif
       }
   }
-  if (!pf_done) prefetch_state();   // threads without records
   HN_BR_T(1);   // region records
   if (n_ovf) {   // this bin's spilled records (bucketed by ovf_place_kernel)
     const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
@@ -2625,7 +2608,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f || !a->fine_src || !a->feat)
     return HN_E_NULL;
   if ((!a->d_table && !a->table_step) || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
-  if (a->d_table_mode != 0 && a->d_table_mode != 1) return HN_E_SHAPE;
+  if (a->d_table_mode < 0 || a->d_table_mode > 3) return HN_E_SHAPE;
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -2675,7 +2658,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     k.bin_cap = bg.cap;
     k.bin_shift = bg.shift;
     k.nbins = bg.nbins;
-  } else if (a->d_table_mode == 1) {
+  } else if (a->d_table_mode & 1) {
     const size_t tb = ((size_t)16 << T) * 2 * sizeof(float);
     if ((st = hip_status(hipMemsetAsync(a->d_table, 0, tb, s)))) return st;
   }
@@ -2718,7 +2701,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.shift = bg.shift;
     r.log2T = T;
     r.d_table = a->d_table;
-    r.overwrite = a->d_table_mode == 1;
+    r.overwrite = (a->d_table_mode & 1) != 0;
     r.fused = a->table_step != nullptr;
     if (r.fused) r.step = *a->table_step;
     hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
@@ -2760,6 +2743,6 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   }
 #endif
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,
-                     a->d_coarse, a->d_fine);
+                     a->d_coarse, a->d_fine, (a->d_table_mode & 2) ? 1 : 0);
   return hip_status(hipGetLastError());
 }

@@ -18,14 +18,18 @@ from . import _lib as L
 
 class KernelTimer:
     """Optional HIP-event timing of the fused launches (bench.py): events are
-    recorded on the same stream the kernels are enqueued on."""
+    recorded on the same stream the kernels are enqueued on.  ``names``
+    limits the timed launches (None: all); each recorded event idles the
+    device for ~5 us, so bench times only what its line reports from the
+    timed steps."""
 
     def __init__(self):
         self.events = {}
         self.enabled = False
+        self.names = None
 
     def begin(self, name):
-        if not self.enabled:
+        if not self.enabled or (self.names is not None and name not in self.names):
             return None
         e = torch.cuda.Event(enable_timing=True)
         e.record()
@@ -254,10 +258,12 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     return out, st
 
 
-def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None):
+def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
+               overwrite_mlp: bool = False):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
-    NeRFSmall weight gradients into dws (coarse 5, fine 5, +=).  grads: any
+    NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
+    overwrite_mlp=True, dws need not be zeroed).  grads: any
     of g_rgb, g_depth, g_acc, g_sparsity, g_rgb0, g_depth0, g_acc0,
     g_sparsity0, g_raw_f (missing = 0).  table_step = (table, exp_avg,
     exp_avg_sq, coeffs) from RAdam.take_step: the binned owner pass applies
@@ -283,7 +289,7 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     a.fine_src = st.fine_src.data_ptr()
     a.feat = st.feat.data_ptr()
     a.weights_packed = 1               # same workspace and weights as the forward
-    a.d_table_mode = 1 if overwrite else 0
+    a.d_table_mode = (1 if overwrite else 0) | (2 if overwrite_mlp else 0)
     a.d_coarse = L.make_mlp_grad(dws[:5])
     a.d_fine = L.make_mlp_grad(dws[5:])
     step = None

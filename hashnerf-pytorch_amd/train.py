@@ -370,19 +370,21 @@ class Trainer:
         lo = HF.loss_fwd(out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts)
         g_rgb, g_rgb0, g_sp, g_sp0, g_tv = HF.loss_bwd(out["rgb"], out["rgb0"], target,
                                                        0 if tv is None else tv.numel(), *consts, self._one)
-        self._gws[0]._base.zero_()                      # the ten MLP grads share one flat buffer
+        # the ten MLP grads (one flat buffer) are written, not accumulated:
+        # no zero fill
         grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)
         if self.fuse_table_step and self.world == 1 and tv is None and self._binned:
             # one GPU, no TV term: the table gradient is complete where the
             # binned owner pass forms it, so the table's RAdam step runs there
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
-            HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table))
+            HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
+                          overwrite_mlp=True)
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
             # no zero fill of the 64 MiB buffer); TV then accumulates into it
-            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True)
+            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True)
             if tv is not None:
                 HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
             table.grad = self._gtable

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 7
+#define HN_ABI_VERSION 8
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -185,8 +185,9 @@ typedef struct hn_render_bwd_args {
   const float* feat;        /* from the forward (saved hash features) */
   int32_t weights_packed;   /* nonzero: `workspace` is the one hn_render_fwd used and the weights
                                are unchanged since, so its packed MFMA copies are reused */
-  int32_t d_table_mode;     /* 0: d_table += gradient (as every d* output); 1: d_table = gradient
-                               (every entry written, the caller need not zero it) */
+  int32_t d_table_mode;     /* bit 0 clear: d_table += gradient (as every d* output); set: d_table =
+                               gradient (every entry written, the caller need not zero it).
+                               bit 1 set: d_coarse / d_fine = their gradients likewise (ABI 8) */
   /* upstream grads (NULL = 0) */
   const float* g_rgb; const float* g_depth; const float* g_acc; const float* g_sparsity;
   const float* g_rgb0; const float* g_depth0; const float* g_acc0; const float* g_sparsity0;

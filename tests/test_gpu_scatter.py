@@ -9,7 +9,8 @@ run_nerf_helpers.py:538-558):
   gradients to 1e-4 (the two schedules sum the tiles' dW in different orders);
 * the binned table gradient is bitwise reproducible (integer sums), the
   atomic one is not required to be;
-* d_table_mode=1 (overwrite) over garbage equals += into zeros;
+* d_table_mode=1 (overwrite) over garbage equals += into zeros; bit 1 does
+  the same for the MLP gradients;
 * a small region capacity (cfg.bin_cap=64) pushes the hot bins' records
   through the shared overflow records: same gradient, no device fault;
 * clumped input (a +-1 box inside the 2..6 sample range, bench config 5:
@@ -63,10 +64,13 @@ def _state(hn, B, T, seed, scatter, bin_cap=0, box=BOX):
     return HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads
 
 
-def _bwd(HF, emb, ws, st, grads, overwrite=False, init=None):
+def _bwd(HF, emb, ws, st, grads, overwrite=False, init=None, mlp_junk=False):
     d_table = torch.zeros_like(emb.table) if init is None else init.clone()
     dws = HF.zeros_like_all(ws)
-    HF.render_bwd(st, grads, d_table, dws, overwrite=overwrite)
+    if mlp_junk:
+        for d in dws:
+            d.fill_(float("nan"))
+    HF.render_bwd(st, grads, d_table, dws, overwrite=overwrite, overwrite_mlp=mlp_junk)
     torch.cuda.synchronize()
     HF.L.check_device_faults()
     return d_table, dws
@@ -97,6 +101,14 @@ def test_binned_bitwise_reproducible_and_overwrite(hn):
     base = torch.randn_like(emb.table)
     t4, _ = _bwd(HF, emb, ws, st, grads, init=base)
     assert torch.equal(t4, base + t1), "d_table_mode=0 adds the gradient once"
+    # d_table_mode bit 1: the MLP gradients are written over NaN garbage; the
+    # dW sums' order varies between launches (tiles per wave), so compare to
+    # += into zeros within fp32 summation noise
+    _, w5 = _bwd(HF, emb, ws, st, grads, mlp_junk=True)
+    _, w6 = _bwd(HF, emb, ws, st, grads)
+    for x, y in zip(w5, w6):
+        assert torch.isfinite(x).all()
+        assert _rel(x, y) <= 1e-5, _rel(x, y)
 
 
 def test_binned_overflow_records(hn):
