@@ -409,7 +409,9 @@ constexpr int kQ = HN_COMPACT ? 512 : 0;
 constexpr int kSyncInts = 5 + 2 * kSlots;
 constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + 2 * kQ + kGsLds + kSyncInts;
 static_assert(kB1LdsF * 4 <= 160 * 1024, "LDS budget");
-static_assert(kB1Img >= W_END, "final dW reduction reuses the images");
+// dW slabs in the workspace: [kBwdBlocks][kSlabSlots][W_END], slot 0 the
+// block's coarse dW, slots 1-3 its fine MLP waves' dW (slab_reduce_kernel)
+constexpr int kSlabSlots = 4;
 static_assert(kRRows * kXS % 4 == 0 && kXS % 4 == 0 && kSlotF % 4 == 0, "b128 alignment");
 
 struct DW {
@@ -2052,7 +2054,7 @@ void render_bwd_kernel(B1K k) {
           if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
-      dw_flush<true>(dw, k.slab + (size_t)blockIdx.x * 2 * W_END, lane);
+      dw_flush<true>(dw, k.slab + (size_t)blockIdx.x * kSlabSlots * W_END, lane);   // slot 0: coarse
       dw_zero(dw);
     }
     // split: wave 0 has the block's 2 * n_rays coarse tiles, waves 1-3 share
@@ -2067,17 +2069,14 @@ void render_bwd_kernel(B1K k) {
         b1_unit<kSf, MODE>(k, block_ray(u / 3), u % 3, X, dw, wr, &ring, pc, &sync[0], u / 3 + 1);
       }
     }
-    // block reduction of the MLP waves' fine dW into wave 0's image, inside
-    // this branch: the accumulators must not be live in the scatter wave's
-    // code (a spill there would wait vmcnt(0), i.e. drain its atomics)
-    if (wave == 0) {
-      for (int j = lane; j < W_END; j += 64) smem[j] = 0.f;
-      ring_publish(&sync[3], 1);
-    }
-    if (!SPLIT || wave != 0) {
-      spin_until(&sync[3], 1, kFaultDwBuf);
-      dw_flush<false>(dw, smem, lane);
-    }
+    // every fine MLP wave stores its fine dW to its own slab slot (split:
+    // waves 1-3 -> slots 1-3; fused: waves 0-2 -> slots 1-3), inside this
+    // branch: the accumulators must not be live in the scatter wave's code (a
+    // spill there would wait vmcnt(0), i.e. drain its atomics).  Formerly the
+    // waves summed into one LDS image with LDS atomics after waiting for wave
+    // 0: ~0.1 M cycles of the kernel's tail.
+    if (!SPLIT || wave != 0)
+      dw_flush<true>(dw, k.slab + ((size_t)blockIdx.x * kSlabSlots + (SPLIT ? wave : wave + 1)) * W_END, lane);
   }
 #if HN_PROFILE
   if (lane == 0 && wave < kMW) {
@@ -2089,31 +2088,37 @@ void render_bwd_kernel(B1K k) {
     atomicAdd(&g_phase[role][4], 1ull);
   }
 #endif
-  __syncthreads();
-  float* slab = k.slab + ((size_t)blockIdx.x * 2 + 1) * W_END;
-  for (int j = threadIdx.x; j < W_END; j += blockDim.x) slab[j] = smem[j];
 }
 
-// dW(coarse) += sum_b slab[b][0], dW(fine) += sum_b slab[b][1].  64
-// consecutive elements per block, kSlabGroups slab-groups per element (8
-// loads in flight per thread, ~18 waves per CU: the 19 MB read is latency
-// bound otherwise), LDS combine in a fixed order, so the sums are
-// deterministic.
+// dW(coarse) (+)= sum_b slab[b][0], dW(fine) (+)= sum_b (slab[b][1] +
+// slab[b][2] + slab[b][3]).  64 consecutive elements per block, kSlabGroups
+// slab-groups per element (8 loads in flight per thread, ~18 waves per CU: the
+// read is latency bound otherwise), LDS combine in a fixed order, so the sums
+// are deterministic given the slabs.
 constexpr int kSlabGroups = 16;
-__global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_slabs,
+__global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_blocks,
                                                                        hn_mlp_grad dc, hn_mlp_grad df, int overwrite) {
   __shared__ float part[kSlabGroups][64];
   const int lane = threadIdx.x & 63;
   const int e = blockIdx.x * 64 + lane;
   const int grp = threadIdx.x >> 6;
+  const bool fine = e >= W_END;
+  const int i = fine ? e - W_END : e;
+  // the slabs summed for this element: (block, slot) pairs, slot 0 (coarse)
+  // or 1..3 (fine), flattened
+  const int per = fine ? kSlabSlots - 1 : 1, n_slabs = n_blocks * per;
+  auto slab_at = [&](int q) {
+    const int b = q / per, slot = fine ? 1 + q % per : 0;
+    return slab[((size_t)b * kSlabSlots + slot) * W_END + i];
+  };
   float s = 0.f;
   if (e < 2 * W_END) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int b = grp;
-    for (; b + 7 * kSlabGroups < n_slabs; b += 8 * kSlabGroups)
+    int q = grp;
+    for (; q + 7 * kSlabGroups < n_slabs; q += 8 * kSlabGroups)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += slab[(size_t)(b + kSlabGroups * q) * 2 * W_END + e];
-    for (; b < n_slabs; b += kSlabGroups) acc[0] += slab[(size_t)b * 2 * W_END + e];
+      for (int u = 0; u < 8; ++u) acc[u] += slab_at(q + kSlabGroups * u);
+    for (; q < n_slabs; q += kSlabGroups) acc[0] += slab_at(q);
     s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
   part[grp][lane] = s;
@@ -2127,8 +2132,6 @@ __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const flo
 #pragma unroll
     for (int g = 0; g < w; ++g) t[g] = t[g] + t[g + w];
   s = t[0];
-  const bool fine = e >= W_END;
-  const int i = fine ? e - W_END : e;
   const hn_mlp_grad& d = fine ? df : dc;
   float* dst;
   if (i < W_S1) dst = d.sigma0 + i;
@@ -2517,7 +2520,7 @@ struct WsLayout {
 static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
-  w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * 2 * W_END + n * kSc * 32 + n * (kSc + kSf) * 4;
+  w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kSc * 32 + n * (kSc + kSf) * 4;
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -2615,7 +2618,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
-  float* dfeat = slab + (size_t)kBwdBlocks * 2 * W_END;
+  float* dfeat = slab + (size_t)kBwdBlocks * kSlabSlots * W_END;
   float* draw = dfeat + (size_t)a->n_rays * kSc * 32;
   if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   B1K k;

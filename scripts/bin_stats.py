@@ -56,7 +56,7 @@ def main():
     st = cap_st["st"]
     n, T = a.n_rand, a.log2T
     shift, nbins, cap = bin_geom(T, n)
-    off = 2 * G_END + BLOCKS * 2 * W_END + n * 64 * 32 + n * 256 * 4
+    off = 2 * G_END + BLOCKS * 4 * W_END + n * 64 * 32 + n * 256 * 4
     off += n * 192 * 32                       # fine feature grads (binned schedule)
     nrec = BLOCKS * nbins * cap + n * 192 * 64   # regions + overflow (ovf_records)
     ws = st.wsb.view(torch.int32)
