@@ -1441,7 +1441,7 @@ struct ScK {
   const float* z_fine;
   const uint8_t* fine_src;
   const float* dfeat_f;   // [B][6][1024] tile order (split render_bwd_kernel)
-  const float* dfeat_c;   // [B][64][32] [f][level] (coarse units)
+  const float* dfeat_c;   // [B][2][1024] tile order (coarse units of the split render_bwd_kernel)
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
 };
@@ -1503,13 +1503,20 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       }
     const int src = k.fine_src[ray * kSf + i];
     if (src < kSc) {                              // coarse twin: fine + coarse grads
-      const f32x4* tw = reinterpret_cast<const f32x4*>(k.dfeat_c + ((size_t)ray * kSc + src) * 32);
+      const f32x4* tw = reinterpret_cast<const f32x4*>(k.dfeat_c + ((size_t)ray * (kSc / 32) + (src >> 5)) * 1024);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const f32x4 q = tw[c];
-        float* d = &gf[c >> 2][4 * (c & 3)];
-        d[0] = d[0] + q.x; d[1] = d[1] + q.y; d[2] = d[2] + q.z; d[3] = d[3] + q.w;
-      }
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f32x4 q = tw[64 * c + 32 * h + (src & 31)];
+          const float e[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int reg = 4 * c + j;
+            float& d = gf[reg & 1][tile_level(reg >> 1, h)];
+            d = d + e[j];
+          }
+        }
     }
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
@@ -1853,9 +1860,16 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
       ring_put(k, *ring, X, r, ray, zq[t], srcq[t], dfeat);
 #endif
       HN_LAP(pc, scat);
+    } else if constexpr (MODE == kModeSplit) {
+      // coarse, split backward: the tile's feature grads in the saved-feature
+      // tile order like the fine tiles (4 coalesced dwordx4 stores; the
+      // per-point layout below took 16 scattered 4-B stores per lane and tile)
+      f32x4* dst = reinterpret_cast<f32x4*>(k.dfeat + ((size_t)ray * (kSc / 32) + tile0 + t) * 1024);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[64 * c + lane] = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
     } else {
-      // coarse: per-point feature grads [point][feature f][level] for the fine
-      // kernel's scatter (lane half h holds levels tile_level(m, h))
+      // coarse, fused backward: per-point feature grads [point][feature f][level]
+      // for the fine units' ring hand-off (lane half h holds levels tile_level(m, h))
       float* dst = k.dfeat + ((size_t)ray * kSc + qbase + p) * 32;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
