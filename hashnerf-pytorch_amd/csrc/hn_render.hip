@@ -1446,7 +1446,12 @@ struct ScK {
   int32_t bin_cap, bin_shift, nbins;
 };
 constexpr int kScWaves = 16;
-constexpr int kScMaxBins = 8192;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
+constexpr int kScMaxBinsLog2 = 13;
+constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
+#ifndef HN_BIN_SHIFT_DEFAULT
+#define HN_BIN_SHIFT_DEFAULT 13
+#endif
+constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per bin (bin_geom)
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __shared__ uint32_t bcnt[kScMaxBins];
@@ -2495,7 +2500,15 @@ struct BinGeom {
 };
 static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   BinGeom g;
-  g.shift = T + 4 < 13 ? T + 4 : 13;
+  static const int env_shift = [] {   // HN_BIN_SHIFT: bin size 2^12 or 2^13 entries
+    const char* e = getenv("HN_BIN_SHIFT");
+    const int v = e ? atoi(e) : 0;
+    return v == 12 || v == 13 ? v : kBinShift;
+  }();
+  // 2^12-entry bins (64 KiB of accumulators: two owner workgroups per CU)
+  // unless that needs more bins than the scatter's LDS counters hold
+  const int want = T + 4 - env_shift <= kScMaxBinsLog2 ? env_shift : 13;
+  g.shift = T + 4 < want ? T + 4 : want;
   g.nbins = 1 << (T + 4 - g.shift);
   const double rpb = (double)((n_rays + kBwdBlocks - 1) / kBwdBlocks);
   const double avg = rpb * (kSf * 4) * ldexp(1.0, g.shift - T);
