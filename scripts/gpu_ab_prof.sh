@@ -15,5 +15,6 @@ for V in "$@"; do
   env $V timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline ${BENCH_ARGS} \
       > $OUT/bench_${TAG}_$i.json 2> $OUT/bench_${TAG}_$i.err || { echo "bench $i failed"; tail -5 $OUT/bench_${TAG}_$i.err; exit 1; }
   python -c "import json;d=json.load(open('$OUT/bench_${TAG}_$i.json'));print('variant $i [$V]', d['value'], d['ms_per_step'], d['kernels'])"
-  env $V bash scripts/gpu_tailprof.sh ${TAG}_$i | head -8 || exit 1
+  env $V bash scripts/gpu_tailprof.sh ${TAG}_$i > $OUT/tail_${TAG}_$i.txt || exit 1
+  head -7 $OUT/tail_${TAG}_$i.txt
 done
