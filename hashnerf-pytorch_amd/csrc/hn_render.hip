@@ -1431,6 +1431,9 @@ HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], 
 #ifndef HN_SC_BATCH      // 1: the 4 corner rows' slot round trips before their stores
 #define HN_SC_BATCH 1
 #endif
+#ifndef HN_SC_LANEMAX    // 1: per-level maxima kept per lane in LDS, reduced once per block
+#define HN_SC_LANEMAX 0
+#endif
 #ifndef HN_SC_DIAG       // diagnostics (wrong gradients): 1 no record stores, 2 also no slot counters
 #define HN_SC_DIAG 0
 #endif
@@ -1457,6 +1460,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __shared__ uint32_t bcnt[kScMaxBins];
   __shared__ float gsl[kGsLds], lvmx[16];
   __shared__ uint32_t lovf;
+#if HN_SC_LANEMAX
+  __shared__ uint32_t lvmxl[16 * 64];
+  for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) lvmxl[i] = 0u;
+#endif
   const int wave = threadIdx.x >> 6, lane = lane_id();
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
   if (threadIdx.x < 16) lvmx[threadIdx.x] = 0.f;
@@ -1563,13 +1570,27 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) rec_store(bw, rs[c], v[c]);
       }
+#if HN_SC_LANEMAX   // per-lane maxima in LDS (one conflict-free ds_max per level), reduced once per block
+      __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
       vmax = wave_max_f32(vmax);
       if (lane == 0)
         __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     }
   }
   __syncthreads();
+#if HN_SC_LANEMAX
+  if (wave == 0) {   // lane = level: the max of its 64 lane slots
+    const int l = lane & 15, q = lane >> 4;
+    uint32_t m = 0u;
+    for (int j = 0; j < 16; ++j) m = max(m, lvmxl[l * 64 + 16 * q + j]);
+    __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __syncthreads();
+#endif
   uint32_t* cnt = bw.idx + nrec + blockIdx.x;
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
     const uint32_t c = bcnt[i];
@@ -2203,6 +2224,10 @@ constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2
 #define HN_BR_PF 0
 #endif
 static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
+#ifndef HN_BR_DEPTH   // records per thread and fetch group (two groups in flight)
+#define HN_BR_DEPTH 4
+#endif
+constexpr int kBrDepth = HN_BR_DEPTH;
 #ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
 #define HN_BR_DIAG 0
 #endif
@@ -2380,9 +2405,9 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   // a binary search over the regions' prefix (measured faster than one search
   // per 4 lane-consecutive records with their 64-B-strided loads); the next
   // 4 records are loaded before the current ones are added (8 in flight)
-  auto fetch = [&](uint32_t r0, f32x4 (&v)[4], uint32_t (&w)[4]) {
+  auto fetch = [&](uint32_t r0, f32x4 (&v)[kBrDepth], uint32_t (&w)[kBrDepth]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kBrDepth; ++q) {
       const uint32_t r = r0 + q * kBinThreads;
       if (r < total) {
         int lo = 0;   // largest p with pre[p] <= r
@@ -2395,33 +2420,28 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       }
     }
   };
-  f32x4 va[4], vb[4];
-  uint32_t wa[4], wb[4];
-  uint32_t r0 = threadIdx.x;
-  if (r0 < total) fetch(r0, va, wa);
-  for (; r0 < total; r0 += 8 * kBinThreads) {
-    const uint32_t r1 = r0 + 4 * kBinThreads;
-    if (r1 < total) fetch(r1, vb, wb);
+  auto add = [&](uint32_t r0, const f32x4 (&v)[kBrDepth], const uint32_t (&w)[kBrDepth]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < kBrDepth; ++q)
       if (r0 + q * kBinThreads < total) {
 #if HN_BR_DIAG == 1   // diagnostic: record loads only
-        if (va[q].x == 1234.5f && wa[q] == 7u) acc[threadIdx.x] = 1ull;
+        if (v[q].x == 1234.5f && w[q] == 7u) acc[threadIdx.x] = 1ull;
 #else
-        bin_add(acc, se, va[q], wa[q], sel, tmask, scale);
+        bin_add(acc, se, v[q], w[q], sel, tmask, scale);
 #endif
       }
+  };
+  f32x4 va[kBrDepth], vb[kBrDepth];
+  uint32_t wa[kBrDepth], wb[kBrDepth];
+  uint32_t r0 = threadIdx.x;
+  if (r0 < total) fetch(r0, va, wa);
+  for (; r0 < total; r0 += 2 * kBrDepth * kBinThreads) {
+    const uint32_t r1 = r0 + kBrDepth * kBinThreads;
+    if (r1 < total) fetch(r1, vb, wb);
+    add(r0, va, wa);
     if (r1 >= total) break;
-    if (r1 + 4 * kBinThreads < total) fetch(r1 + 4 * kBinThreads, va, wa);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (r1 + q * kBinThreads < total) {
-#if HN_BR_DIAG == 1
-        if (vb[q].x == 1234.5f && wb[q] == 7u) acc[threadIdx.x] = 1ull;
-#else
-        bin_add(acc, se, vb[q], wb[q], sel, tmask, scale);
-#endif
-      }
+    if (r1 + kBrDepth * kBinThreads < total) fetch(r1 + kBrDepth * kBinThreads, va, wa);
+    add(r1, vb, wb);
   }
   HN_BR_T(1);   // region records
   if (n_ovf) {   // this bin's spilled records (bucketed by ovf_place_kernel)
