@@ -532,7 +532,18 @@ constexpr GemmSeg kSegs[] = {{R_F0, 0}, {R_F0, 1}, {R_F1, 0}, {R_F2G, 0}, {R_F2G
                              {R_B0, 0}};
 #endif
 constexpr int kNSegs = sizeof(kSegs) / sizeof(kSegs[0]);
-constexpr int seg_groups(const GemmSeg& g) { return reg_gpo(g.r) * (g.ob < 0 ? 2 : 1); }
+// HN_SPLIT_R: parts the backward's forward recompute uses of the forward
+// regions' HN_SPLIT_F packed parts (the leading parts of a split are the same
+// for every part count, so the recompute streams only groups q < HN_SPLIT_R of
+// each chunk).  3 = the forward's own products (bit-identical activations).
+#ifndef HN_SPLIT_R
+#define HN_SPLIT_R 3
+#endif
+constexpr int seg_ns(const GemmSeg& g) {   // parts this stream uses per chunk (0: f32)
+  return g.r < R_B4 && reg_ns(g.r) > HN_SPLIT_R ? HN_SPLIT_R : reg_ns(g.r);
+}
+constexpr int seg_gpo(const GemmSeg& g) { return seg_ns(g) ? seg_ns(g) * kRegKS[g.r] / 8 : kRegKS[g.r] / 4; }
+constexpr int seg_groups(const GemmSeg& g) { return seg_gpo(g) * (g.ob < 0 ? 2 : 1); }
 constexpr int seg_start(int i) {   // first group of segment i in the stream
   int n = 0;
   for (int j = 0; j < i; ++j) n += seg_groups(kSegs[j]);
@@ -549,20 +560,21 @@ constexpr int group_off(int idx) {
   idx %= kTilePeriod;
   if (idx >= kTileGroups) idx = 0;              // pad groups re-read group 0
   for (const GemmSeg& g : kSegs) {
-    const int n = reg_gpo(g.r);
+    const int n = reg_gpo(g.r), u = seg_gpo(g);   // packed / streamed groups per block
+    const int per = seg_ns(g) ? seg_ns(g) : 1, pk = reg_ns(g.r) ? reg_ns(g.r) : 1;   // per chunk
     if (g.ob >= 0) {
-      if (idx < n) return reg_off(g.r) + (g.ob * n + idx) * 256;
-    } else if (idx < 2 * n) {
-      const int per = reg_ns(g.r) ? reg_ns(g.r) : 1;   // groups per chunk and block
+      if (idx < u) return reg_off(g.r) + (g.ob * n + pk * (idx / per) + idx % per) * 256;
+    } else if (idx < 2 * u) {
       const int c = idx / (2 * per), ob = idx / per % 2, q = idx % per;
-      return reg_off(g.r) + (ob * n + per * c + q) * 256;
+      return reg_off(g.r) + (ob * n + pk * c + q) * 256;
     }
     idx -= seg_groups(g);
   }
   return 0;
 }
 static_assert(group_off(kTileGroups - 1) == G_B0 + (reg_gpo(R_B0) - 1) * 256, "GEMM sequence");
-static_assert(HN_SPLIT_F != 3 || HN_SPLIT_FC != 3 || HN_SPLIT_B != 2 || (kTileGroups == 92 && G_END == 30208), "layout");
+static_assert(HN_SPLIT_F != 3 || HN_SPLIT_FC != 3 || HN_SPLIT_B != 2 || HN_SPLIT_R != 3 ||
+              (kTileGroups == 92 && G_END == 30208), "layout");
 
 struct WRing {
   f32x4 b[kRing];
@@ -609,7 +621,7 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
 // quad offset F4B + 4 (c % 2) (put_parts; Xb = the wave's images).
 template <int SEG, int IMG = -1, int F4B = 0, typename BF>
 HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, char* Xb = nullptr) {
-  constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = reg_ns(R), START = seg_start(SEG);
+  constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
   if constexpr (NS > 0) {                       // split-f32: NS groups per K = 16 chunk
     static_for<0, KS / 8>([&](auto cc) {
@@ -640,7 +652,7 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
 // chunk for both blocks, and two independent accumulator chains
 template <int SEG, int IMG = -1, int F4B = 0, typename BF>
 HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int lane, BF bval, char* Xb = nullptr) {
-  constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = reg_ns(R), START = seg_start(SEG);
+  constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(kSegs[SEG].ob < 0, "paired segment");
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
   if constexpr (NS > 0) {
@@ -1432,7 +1444,7 @@ HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], 
 #define HN_SC_BATCH 1
 #endif
 #ifndef HN_SC_LANEMAX    // 1: per-level maxima kept per lane in LDS, reduced once per block
-#define HN_SC_LANEMAX 0
+#define HN_SC_LANEMAX 1
 #endif
 #ifndef HN_SC_DIAG       // diagnostics (wrong gradients): 1 no record stores, 2 also no slot counters
 #define HN_SC_DIAG 0
