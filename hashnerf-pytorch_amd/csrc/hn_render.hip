@@ -1459,7 +1459,11 @@ struct ScK {
   const float* dfeat_c;   // [B][2][1024] tile order (coarse units of the split render_bwd_kernel)
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
+  int32_t scramble;       // render_bwd_kernel's Feistel half-width (HN_SC_PERM), 0: identity
 };
+#ifndef HN_SC_PERM       // 1: a block's rays through the backward's batch permutation
+#define HN_SC_PERM 0
+#endif
 constexpr int kScWaves = 16;
 constexpr int kScMaxBinsLog2 = 13;
 constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
@@ -1502,7 +1506,20 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int64_t u1 = u0 + per < units ? u0 + per : units;
   const int pp = lane & 15;
   for (int64_t u = u0 + wave; u < u1; u += kScWaves) {
+#if HN_SC_PERM
+    // the block's rays spread over the (spatially ordered) batch: fewer
+    // same-entry records per region at the coarse levels
+    int64_t ray = u / 3;
+    if (k.scramble) {
+      uint32_t x = (uint32_t)ray;
+      do {
+        x = feistel(x, k.scramble, 0x5bd1e995u);
+      } while ((int64_t)x >= k.B);
+      ray = (int64_t)x;
+    }
+#else
     const int64_t ray = u / 3;
+#endif
     const int i = 64 * (int)(u % 3) + lane;       // fine sample
     Ray r;
     load_ray(k.rays, ray, r);
@@ -2259,9 +2276,18 @@ HN_DEV long long fx_of(float v, float scale) {
 // wave's random entries spread over twice the LDS banks of [entry][feature])
 HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_t w, uint32_t sel,
                     uint32_t tmask, float scale) {
+#if HN_BR_DIAG == 2   // diagnostic: entries scrambled per lane (no same-address serialisation; wrong gradient)
+  const uint32_t e0 = ((w & 0x0fffffffu) ^ (__lane_id() * 97u)) & sel;
+#else
   const uint32_t e0 = w & 0x0fffffffu & sel;
+#endif
   const uint32_t e1 = e0 ^ (((1u << (w >> 28)) - 1u) & tmask);
+#if HN_BR_DIAG == 3   // diagnostic: no fixed-point conversion (wrong gradient)
+  const long long q[4] = {(long long)__float_as_int(v.x), (long long)__float_as_int(v.y),
+                          (long long)__float_as_int(v.z), (long long)__float_as_int(v.w)};
+#else
   const long long q[4] = {fx_of(v.x, scale), fx_of(v.y, scale), fx_of(v.z, scale), fx_of(v.w, scale)};
+#endif
   __hip_atomic_fetch_add(acc + e0, (unsigned long long)q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_add(acc + se + e0, (unsigned long long)q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_add(acc + e1, (unsigned long long)q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2751,6 +2777,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.bin_cap = k.bin_cap;
     sk.bin_shift = k.bin_shift;
     sk.nbins = k.nbins;
+    sk.scramble = k.scramble;
     hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), 0, s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
