@@ -1309,9 +1309,21 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // that each owner reads only its own.
 enum : int { kFaultBins = 16 };
 
+// Record r in memory (HN_REC_AOS 1): groups of 4 records = 4 value quads
+// then their 4 entry words (80 B), so a record's value and word share a line
+// and a region is one contiguous stream (the scatter's partially written L2
+// lines and the owner's DRAM chunks per region are halved); HN_REC_AOS 0: the
+// values [nrec] f32x4 then the words [nrec] u32.  Either way the records take
+// 5 * nrec floats from `bins` and the book words follow at bins + 5 * nrec
+// (ovf_book's idx base = bins + 4 * nrec).
+#ifndef HN_REC_AOS
+#define HN_REC_AOS 1
+#endif
+HN_DEV size_t rec_vofs(size_t r) { return HN_REC_AOS ? (r >> 2) * 20 + (r & 3) * 4 : 4 * r; }
+HN_DEV size_t rec_wofs(size_t r, size_t nrec) { return HN_REC_AOS ? (r >> 2) * 20 + 16 + (r & 3) : 4 * nrec + r; }
 struct BinW {
-  f32x4* vals;
-  uint32_t* idx;
+  float* bins;
+  size_t nrec;
   uint32_t* lcnt;      // LDS [nbins] record counts
   uint32_t* lovf;      // LDS: this block's overflow records
   size_t base;         // first record of this block's region of bin 0
@@ -1408,8 +1420,8 @@ HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
   ok = ok && v[0] == 1234.5f && v[1] == 5432.1f;
 #endif
   if (ok) {
-    bw.vals[r] = f32x4{v[0], v[1], v[2], v[3]};
-    bw.idx[r] = rs.word;
+    *reinterpret_cast<f32x4*>(bw.bins + rec_vofs(r)) = f32x4{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<uint32_t*>(bw.bins)[rec_wofs(r, bw.nrec)] = rs.word;
   }
 }
 
@@ -1488,9 +1500,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __syncthreads();
   BinW bw;
   const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
-  bw.vals = reinterpret_cast<f32x4*>(k.bins);
-  bw.idx = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
-  const OvfBook ob = ovf_book(bw.idx, nrec, k.nbins);
+  bw.bins = k.bins;
+  bw.nrec = nrec;
+  uint32_t* const book = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
+  const OvfBook ob = ovf_book(book, nrec, k.nbins);
   bw.lovf = &lovf;
   bw.n_ovf = (uint32_t)ovf_per_block(k.B);
   bw.lcnt = bcnt;
@@ -1620,14 +1633,14 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
   __syncthreads();
 #endif
-  uint32_t* cnt = bw.idx + nrec + blockIdx.x;
+  uint32_t* cnt = book + nrec + blockIdx.x;
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
     const uint32_t c = bcnt[i];
     cnt[(size_t)i * kBwdBlocks] = c;
     if (c > bw.cap)   // spilled records of bin i (ovf_place_kernel's bucket sizes)
       __hip_atomic_fetch_add(ob.per_bin + i, c - bw.cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  float* mxo = reinterpret_cast<float*>(bw.idx + nrec + (size_t)kBwdBlocks * k.nbins) + blockIdx.x;
+  float* mxo = reinterpret_cast<float*>(book + nrec + (size_t)kBwdBlocks * k.nbins) + blockIdx.x;
   if (threadIdx.x < 16) mxo[threadIdx.x * kBwdBlocks] = lvmx[threadIdx.x];
   if (threadIdx.x == 0) {
     const uint32_t n = lovf < bw.n_ovf ? lovf : bw.n_ovf;
@@ -2338,8 +2351,9 @@ __global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
     }
   }
   const size_t o0 = (size_t)blockIdx.x * ovf_per_block(k.n_rays);   // this list, relative to the overflow
-  const uint32_t* lst = idx + (size_t)kBwdBlocks * k.nbins * k.cap + o0;
-  auto bin_of = [&](uint32_t s) { return (lst[s] & 0x0fffffffu) >> k.shift; };
+  const size_t l0 = (size_t)kBwdBlocks * k.nbins * k.cap + o0;   // first record of this list
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(k.bins);
+  auto bin_of = [&](uint32_t s) { return (words[rec_wofs(l0 + s, nrec)] & 0x0fffffffu) >> k.shift; };
   for (uint32_t s = t; s < mine; s += kPlaceThreads)
     __hip_atomic_fetch_add(lc + bin_of(s), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __syncthreads();
@@ -2396,8 +2410,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   if (HN_BR_PF == 1 && k.fused) load_state();
   for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
-  const f32x4* vals = reinterpret_cast<const f32x4*>(k.bins);
-  const uint32_t* idx = reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec);
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(k.bins);
+  const uint32_t* idx = reinterpret_cast<const uint32_t*>(k.bins + 4 * nrec);   // book base
   const uint32_t* cnt = idx + nrec;
   const float* mxs = reinterpret_cast<const float*>(cnt + (size_t)kBwdBlocks * k.nbins);   // [16][blocks]
   const OvfBook obk = ovf_book(const_cast<uint32_t*>(idx), nrec, k.nbins);
@@ -2453,8 +2467,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
         for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
           if (pre[lo + st] <= r) lo += st;
         const size_t rec = bbase + (size_t)lo * k.cap + (r - pre[lo]);
-        v[q] = vals[rec];
-        w[q] = idx[rec];
+        v[q] = *reinterpret_cast<const f32x4*>(k.bins + rec_vofs(rec));
+        w[q] = words[rec_wofs(rec, nrec)];
       }
     }
   };
@@ -2487,7 +2501,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     const uint32_t lo = obk.first[b], hi = lo + obk.per_bin[b];
     for (uint32_t s = lo + threadIdx.x; s < hi; s += kBinThreads) {
       const uint32_t o = obk.ids[s];
-      bin_add(acc, se, vals[ob + o], idx[ob + o], sel, tmask, scale);
+      bin_add(acc, se, *reinterpret_cast<const f32x4*>(k.bins + rec_vofs(ob + o)), words[rec_wofs(ob + o, nrec)],
+              sel, tmask, scale);
     }
   }
   __syncthreads();

@@ -81,6 +81,7 @@ def main():
     # 2048 items (entry, owner (e >> 5) & 15); per owner batches of 64 items;
     # the claim rounds a batch needs = max items per tag slot (hashed entry)
     vals_i = off
+    aos = os.environ.get("HN_REC_AOS", "1") != "0"   # the library's build setting
     idx_i = off + 4 * nrec
     wsi = ws
     sel, tmask = (1 << shift) - 1, (1 << T) - 1
@@ -88,8 +89,10 @@ def main():
         c = np.minimum(cnt[b], cap)
         recs = []
         for p in range(BLOCKS):
-            s0 = idx_i + (b * BLOCKS + p) * cap
-            recs.append(wsi[s0:s0 + int(c[p])].cpu().numpy().view(np.uint32))
+            r = (b * BLOCKS + p) * cap + np.arange(int(c[p]))
+            # records in groups of 4 (4 value quads, then 4 words: HN_REC_AOS)
+            wi = vals_i + (r >> 2) * 20 + 16 + (r & 3) if aos else idx_i + r
+            recs.append(wsi[torch.from_numpy(wi).to(wsi.device)].cpu().numpy().view(np.uint32))
         w = np.concatenate(recs)
         e0 = (w & 0x0fffffff) & sel
         d = ((np.uint32(1) << (w >> 28)) - 1) & tmask
