@@ -1309,15 +1309,16 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // that each owner reads only its own.
 enum : int { kFaultBins = 16 };
 
-// Record r in memory (HN_REC_AOS 1): groups of 4 records = 4 value quads
-// then their 4 entry words (80 B), so a record's value and word share a line
-// and a region is one contiguous stream (the scatter's partially written L2
-// lines and the owner's DRAM chunks per region are halved); HN_REC_AOS 0: the
-// values [nrec] f32x4 then the words [nrec] u32.  Either way the records take
+// Record r in memory.  HN_REC_AOS 0 (default): the values [nrec] f32x4 then
+// the words [nrec] u32.  HN_REC_AOS 1: groups of 4 records = 4 value quads
+// then their 4 entry words (80 B), a record's value and word in one line and
+// one write stream per region -- measured slower on config 2 (scatter +5 us,
+// owner +6.5 us, two A/B pairs on one box): the owner's value loads then span
+// 80-B strides instead of dense 1-KiB runs.  Either way the records take
 // 5 * nrec floats from `bins` and the book words follow at bins + 5 * nrec
 // (ovf_book's idx base = bins + 4 * nrec).
 #ifndef HN_REC_AOS
-#define HN_REC_AOS 1
+#define HN_REC_AOS 0
 #endif
 HN_DEV size_t rec_vofs(size_t r) { return HN_REC_AOS ? (r >> 2) * 20 + (r & 3) * 4 : 4 * r; }
 HN_DEV size_t rec_wofs(size_t r, size_t nrec) { return HN_REC_AOS ? (r >> 2) * 20 + 16 + (r & 3) : 4 * nrec + r; }

@@ -81,7 +81,7 @@ def main():
     # 2048 items (entry, owner (e >> 5) & 15); per owner batches of 64 items;
     # the claim rounds a batch needs = max items per tag slot (hashed entry)
     vals_i = off
-    aos = os.environ.get("HN_REC_AOS", "1") != "0"   # the library's build setting
+    aos = os.environ.get("HN_REC_AOS", "0") != "0"   # the library build setting (-DHN_REC_AOS)
     idx_i = off + 4 * nrec
     wsi = ws
     sel, tmask = (1 << shift) - 1, (1 << T) - 1
