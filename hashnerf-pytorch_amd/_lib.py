@@ -119,6 +119,8 @@ SIGNATURES = {
                                 C.c_float, _P, _P]),
     "hn_loss_bwd": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_float, _P,
                                 _P, _P, _P, _P, _P, _P]),
+    "hn_loss_fwd_bwd": (C.c_int32, [_P, _P, _P, _P, _P, C.c_int64, _P, C.c_int32, C.c_float, C.c_float,
+                                    C.c_float, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hn_render_workspace_bytes": (C.c_size_t, [C.POINTER(HnRenderCfg), C.c_int64]),
     "hn_render_scatter_mode": (C.c_int32, [C.POINTER(HnRenderCfg), C.c_int64]),
     "hn_render_fwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderFwdArgs), _P,

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kMortonThreads) void morton_emit_kernel(hn_ray_samp
 // ---------------------------------------------------------------------------
 constexpr int kLossThreads = 1024;
 
-__global__ __launch_bounds__(kLossThreads) void loss_fwd_kernel(
+HN_DEV void loss_fwd_block(
     const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target,
     const float* __restrict__ sp, const float* __restrict__ sp0, int64_t n, const float* __restrict__ tv,
     int n_tv, float world, float sparse_w, float tv_w, float* __restrict__ out) {
@@ -211,18 +211,23 @@ __global__ __launch_bounds__(kLossThreads) void loss_fwd_kernel(
     out[3] = ent;
   }
 }
+__global__ __launch_bounds__(kLossThreads) void loss_fwd_kernel(
+    const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target,
+    const float* __restrict__ sp, const float* __restrict__ sp0, int64_t n, const float* __restrict__ tv,
+    int n_tv, float world, float sparse_w, float tv_w, float* __restrict__ out) {
+  loss_fwd_block(rgb, rgb0, target, sp, sp0, n, tv, n_tv, world, sparse_w, tv_w, out);
+}
 
 // Backward, op for op as autograd evaluates the eager expression:
 //   (mse + mse0) / world   -> g / world (DivBackward)
 //   mean over 3n            -> (.) / 3n  (MeanBackward: expand, divide by numel)
 //   (x - t) ** 2            -> (.) * (2 * (x - t))  (PowBackward)
 //   sparse_w * sum(sp)      -> g * sparse_w;   tv_w * sum(tv) -> g * tv_w
-__global__ __launch_bounds__(256) void loss_bwd_kernel(
-    const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target, int64_t n,
-    int n_tv, float world, float sparse_w, float tv_w, const float* __restrict__ g_loss,
+HN_DEV void loss_bwd_elem(
+    int64_t j, const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target,
+    int64_t n, int n_tv, float world, float sparse_w, float tv_w, const float* __restrict__ g_loss,
     float* __restrict__ g_rgb, float* __restrict__ g_rgb0, float* __restrict__ g_sp, float* __restrict__ g_sp0,
     float* __restrict__ g_tv) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float g = *g_loss;
   const float gm = (g / world) / (float)(3 * n);
   if (j < 3 * n) {
@@ -234,6 +239,29 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     if (g_sp0) g_sp0[j] = g * sparse_w;
   }
   if (g_tv && j < n_tv) g_tv[j] = g * tv_w;
+}
+__global__ __launch_bounds__(256) void loss_bwd_kernel(
+    const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target, int64_t n,
+    int n_tv, float world, float sparse_w, float tv_w, const float* __restrict__ g_loss,
+    float* __restrict__ g_rgb, float* __restrict__ g_rgb0, float* __restrict__ g_sp, float* __restrict__ g_sp0,
+    float* __restrict__ g_tv) {
+  loss_bwd_elem((int64_t)blockIdx.x * blockDim.x + threadIdx.x, rgb, rgb0, target, n, n_tv, world, sparse_w, tv_w,
+                g_loss, g_rgb, g_rgb0, g_sp, g_sp0, g_tv);
+}
+// Both in one launch (the trainer's step): workgroup 0 reduces the loss, the
+// others write the gradients -- the backward does not depend on the loss
+// value, so the two run side by side; results bitwise those of the two kernels.
+__global__ __launch_bounds__(kLossThreads) void loss_fwd_bwd_kernel(
+    const float* __restrict__ rgb, const float* __restrict__ rgb0, const float* __restrict__ target,
+    const float* __restrict__ sp, const float* __restrict__ sp0, int64_t n, const float* __restrict__ tv,
+    int n_tv, float world, float sparse_w, float tv_w, float* __restrict__ out, const float* __restrict__ g_loss,
+    float* __restrict__ g_rgb, float* __restrict__ g_rgb0, float* __restrict__ g_sp, float* __restrict__ g_sp0,
+    float* __restrict__ g_tv) {
+  if (blockIdx.x == 0)
+    loss_fwd_block(rgb, rgb0, target, sp, sp0, n, tv, n_tv, world, sparse_w, tv_w, out);
+  else
+    loss_bwd_elem((int64_t)(blockIdx.x - 1) * kLossThreads + threadIdx.x, rgb, rgb0, target, n, n_tv, world,
+                  sparse_w, tv_w, g_loss, g_rgb, g_rgb0, g_sp, g_sp0, g_tv);
 }
 
 }  // namespace hn
@@ -326,5 +354,20 @@ extern "C" int32_t hn_loss_bwd(const float* rgb, const float* rgb0, const float*
   const unsigned blocks = (unsigned)((m + 255) / 256);
   hipLaunchKernelGGL(loss_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rgb, rgb0, target, n_rays,
                      n_tv, world, sparse_w, tv_w, g_loss, g_rgb, g_rgb0, g_sp, g_sp0, g_tv);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_loss_fwd_bwd(const float* rgb, const float* rgb0, const float* target, const float* sp,
+                                   const float* sp0, int64_t n_rays, const float* tv, int32_t n_tv, float world,
+                                   float sparse_w, float tv_w, float* out, const float* g_loss, float* g_rgb,
+                                   float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv, void* stream) {
+  if (n_rays <= 0 || n_tv < 0) return HN_E_SHAPE;
+  if (!rgb || !target || !sp || !out || !g_loss || !g_rgb) return HN_E_NULL;
+  if ((rgb0 == nullptr) != (sp0 == nullptr) || (rgb0 == nullptr) != (g_rgb0 == nullptr)) return HN_E_NULL;
+  const int64_t m = 3 * n_rays > n_tv ? 3 * n_rays : n_tv;
+  const unsigned blocks = 1u + (unsigned)((m + kLossThreads - 1) / kLossThreads);
+  hipLaunchKernelGGL(loss_fwd_bwd_kernel, dim3(blocks), dim3(kLossThreads), 0, (hipStream_t)stream, rgb, rgb0,
+                     target, sp, sp0, n_rays, tv, n_tv, world, sparse_w, tv_w, out, g_loss, g_rgb, g_rgb0, g_sp,
+                     g_sp0, g_tv);
   return hip_status(hipGetLastError());
 }

@@ -431,6 +431,27 @@ def loss_bwd(rgb, rgb0, target, n_tv, world, sparse_w, tv_w, g_loss, has_sp0=Tru
     return g_rgb, g_rgb0, g_sp, g_sp0, g_tv
 
 
+def loss_fwd_bwd(rgb, rgb0, target, sp, sp0, tv, world, sparse_w, tv_w, g_loss):
+    """hn_loss_fwd_bwd: loss_fwd and loss_bwd in one launch -> (out [4],
+    (g_rgb, g_rgb0, g_sp, g_sp0, g_tv)), bitwise the two calls' results."""
+    L.require_device(rgb, target, sp)
+    n = rgb.shape[0]
+    dev = rgb.device
+    n_tv = 0 if tv is None else tv.numel()
+    out = torch.empty(4, dtype=torch.float32, device=dev)
+    g_rgb = torch.empty_like(rgb)
+    g_rgb0 = torch.empty_like(rgb) if rgb0 is not None else None
+    g_sp = torch.empty(n, dtype=torch.float32, device=dev)
+    g_sp0 = torch.empty(n, dtype=torch.float32, device=dev) if sp0 is not None else None
+    g_tv = torch.empty(n_tv, dtype=torch.float32, device=dev) if n_tv else None
+    L.check(L.lib().hn_loss_fwd_bwd(L.ptr(L.contig(rgb)), L.ptr(L.contig(rgb0)), L.ptr(L.contig(target)),
+                                    L.ptr(L.contig(sp)), L.ptr(L.contig(sp0)), n, L.ptr(L.contig(tv)), n_tv,
+                                    float(world), float(sparse_w), float(tv_w), L.ptr(out),
+                                    L.ptr(g_loss.contiguous()), L.ptr(g_rgb), L.ptr(g_rgb0), L.ptr(g_sp),
+                                    L.ptr(g_sp0), L.ptr(g_tv), L.stream(dev)), "loss_fwd_bwd")
+    return out, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv)
+
+
 class TrainLossFn(torch.autograd.Function):
     """loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * (sum sp + sum sp0) +
     tv_w * sum tv (run_nerf.py:612-636 under train.dp_loss's DP rule).

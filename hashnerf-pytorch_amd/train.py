@@ -367,9 +367,10 @@ class Trainer:
             cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
-        lo = HF.loss_fwd(out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts)
-        g_rgb, g_rgb0, g_sp, g_sp0, g_tv = HF.loss_bwd(out["rgb"], out["rgb0"], target,
-                                                       0 if tv is None else tv.numel(), *consts, self._one)
+        # loss value and its input gradients in one launch (the gradients do
+        # not depend on the value)
+        lo, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(
+            out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts, self._one)
         # the ten MLP grads (one flat buffer) are written, not accumulated:
         # no zero fill
         grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)

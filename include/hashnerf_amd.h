@@ -277,6 +277,13 @@ int32_t hn_loss_fwd(const float* rgb, const float* rgb0, const float* target, co
 int32_t hn_loss_bwd(const float* rgb, const float* rgb0, const float* target, int64_t n_rays,
                     int32_t n_tv, float world, float sparse_w, float tv_w, const float* g_loss,
                     float* g_rgb, float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv, void* stream);
+/* hn_loss_fwd and hn_loss_bwd in one launch (the trainer's step: the backward
+ * does not depend on the loss value); out and the gradients bitwise those of
+ * the two calls. */
+int32_t hn_loss_fwd_bwd(const float* rgb, const float* rgb0, const float* target, const float* sp,
+                        const float* sp0, int64_t n_rays, const float* tv, int32_t n_tv, float world,
+                        float sparse_w, float tv_w, float* out, const float* g_loss, float* g_rgb,
+                        float* g_rgb0, float* g_sp, float* g_sp0, float* g_tv, void* stream);
 
 size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
 /* The table-gradient scatter hn_render_bwd runs for this configuration and

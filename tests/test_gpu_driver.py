@@ -120,6 +120,26 @@ def test_fused_loss_matches_eager(hn, world, tv):
     torch.testing.assert_close(mse0, m0.detach(), rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("world,tv,B", [(1, False, 1000), (2, True, 4096), (1, True, 3)])
+def test_loss_fwd_bwd_one_launch_bitwise(hn, world, tv, B):
+    """hn_loss_fwd_bwd (the trainer's single launch) = hn_loss_fwd + hn_loss_bwd, bitwise."""
+    from hashnerf_pytorch_amd import functional as HF
+    g = torch.Generator().manual_seed(5)
+    mk = lambda *s: torch.rand(s, generator=g).to(DEV)
+    rgb, rgb0, sp, sp0, target = mk(B, 3), mk(B, 3), mk(B), mk(B), mk(B, 3)
+    tvv = mk(5000) if tv else None       # n_tv > 3 B for the small batch: the grid covers it
+    one = torch.ones((), device=DEV)
+    consts = (world, 1e-3, 1e-2)
+    out_a = HF.loss_fwd(rgb, rgb0, target, sp, sp0, tvv, *consts)
+    g_a = HF.loss_bwd(rgb, rgb0, target, 0 if tvv is None else tvv.numel(), *consts, one)
+    out_b, g_b = HF.loss_fwd_bwd(rgb, rgb0, target, sp, sp0, tvv, *consts, one)
+    assert torch.equal(out_a, out_b)
+    for a, b in zip(g_a, g_b):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a, b)
+
+
 def test_trainer_explicit_matches_autograd(hn):
     """The explicit launch sequence (mode="explicit") and the autograd module
     API (mode="autograd") give the same loss and gradients for the same seeds
