@@ -2271,6 +2271,10 @@ static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 en
 #define HN_BR_DEPTH 4
 #endif
 constexpr int kBrDepth = HN_BR_DEPTH;
+#ifndef HN_BR_SEARCH   // 1: a record's region from a per-64-record-chunk table + a forward walk
+#define HN_BR_SEARCH 0
+#endif
+constexpr int kBrChunks = 8192;   // table entries (16 KiB of LDS): bins of up to 512 K records
 #ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
 #define HN_BR_DIAG 0
 #endif
@@ -2452,6 +2456,24 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __syncthreads();
   const uint32_t total = pre[kBwdBlocks];
   const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u, se = 1u << k.shift;
+#if HN_BR_SEARCH
+  // region of the first record of every 64-record chunk: a record's region is
+  // then a short forward walk from its chunk's (regions hold ~24-114 records)
+  // instead of an 8-step binary search
+  __shared__ uint16_t first_reg[kBrChunks];
+  const bool tab = ((total + 63) >> 6) <= (uint32_t)kBrChunks;   // uniform
+  if (tab) {
+    for (uint32_t c = threadIdx.x; c < ((total + 63) >> 6); c += kBinThreads) {
+      const uint32_t r = c << 6;
+      int lo = 0;
+#pragma unroll
+      for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
+        if (pre[lo + st] <= r) lo += st;
+      first_reg[c] = (uint16_t)lo;
+    }
+    __syncthreads();
+  }
+#endif
   HN_BR_T(0);   // accumulator zeroing, counts, prefix, scale
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
   // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found by
@@ -2464,9 +2486,17 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       const uint32_t r = r0 + q * kBinThreads;
       if (r < total) {
         int lo = 0;   // largest p with pre[p] <= r
+#if HN_BR_SEARCH
+        if (tab) {
+          lo = first_reg[r >> 6];
+          while (pre[lo + 1] <= r) ++lo;   // r < total = pre[kBwdBlocks]: stops by lo = 255
+        } else
+#endif
+        {
 #pragma unroll
-        for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
-          if (pre[lo + st] <= r) lo += st;
+          for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
+            if (pre[lo + st] <= r) lo += st;
+        }
         const size_t rec = bbase + (size_t)lo * k.cap + (r - pre[lo]);
         v[q] = *reinterpret_cast<const f32x4*>(k.bins + rec_vofs(rec));
         w[q] = words[rec_wofs(rec, nrec)];
