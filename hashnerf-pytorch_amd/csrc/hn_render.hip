@@ -2272,7 +2272,7 @@ static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 en
 #endif
 constexpr int kBrDepth = HN_BR_DEPTH;
 #ifndef HN_BR_SEARCH   // 1: a record's region from a per-64-record-chunk table + a forward walk
-#define HN_BR_SEARCH 0
+#define HN_BR_SEARCH 1
 #endif
 constexpr int kBrChunks = 8192;   // table entries (16 KiB of LDS): bins of up to 512 K records
 #ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
