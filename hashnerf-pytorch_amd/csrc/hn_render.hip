@@ -2476,10 +2476,11 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #endif
   HN_BR_T(0);   // accumulator zeroing, counts, prefix, scale
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
-  // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found by
-  // a binary search over the regions' prefix (measured faster than one search
-  // per 4 lane-consecutive records with their 64-B-strided loads); the next
-  // 4 records are loaded before the current ones are added (8 in flight)
+  // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found in
+  // the regions' prefix from its 64-record chunk's first region (HN_BR_SEARCH;
+  // else a binary search; both measured faster than one search per 4
+  // lane-consecutive records with their 64-B-strided loads); the next group
+  // of records is loaded before the current one is added
   auto fetch = [&](uint32_t r0, f32x4 (&v)[kBrDepth], uint32_t (&w)[kBrDepth]) {
 #pragma unroll
     for (int q = 0; q < kBrDepth; ++q) {
