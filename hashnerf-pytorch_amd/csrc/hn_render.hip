@@ -2179,6 +2179,10 @@ void render_bwd_kernel(B1K k) {
 // read is latency bound otherwise), LDS combine in a fixed order, so the sums
 // are deterministic given the slabs.
 constexpr int kSlabGroups = 16;
+#ifndef HN_SLAB_ILP   // slab loads in flight per thread (a power of 2)
+#define HN_SLAB_ILP 8
+#endif
+constexpr int kSlabIlp = HN_SLAB_ILP;
 __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_blocks,
                                                                        hn_mlp_grad dc, hn_mlp_grad df, int overwrite) {
   __shared__ float part[kSlabGroups][64];
@@ -2196,13 +2200,19 @@ __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const flo
   };
   float s = 0.f;
   if (e < 2 * W_END) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int q = grp;
-    for (; q + 7 * kSlabGroups < n_slabs; q += 8 * kSlabGroups)
+    float acc[kSlabIlp];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc[u] += slab_at(q + kSlabGroups * u);
+    for (int u = 0; u < kSlabIlp; ++u) acc[u] = 0.f;
+    int q = grp;
+    for (; q + (kSlabIlp - 1) * kSlabGroups < n_slabs; q += kSlabIlp * kSlabGroups)
+#pragma unroll
+      for (int u = 0; u < kSlabIlp; ++u) acc[u] += slab_at(q + kSlabGroups * u);
     for (; q < n_slabs; q += kSlabGroups) acc[0] += slab_at(q);
-    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+    for (int w = kSlabIlp / 2; w >= 1; w /= 2)   // pairwise, fixed order
+#pragma unroll
+      for (int u = 0; u < w; ++u) acc[u] = acc[u] + acc[u + w];
+    s = acc[0];
   }
   part[grp][lane] = s;
   __syncthreads();
