@@ -2634,6 +2634,10 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   }();
   if (cap_override <= 0) cap_override = env_cap;
   g.cap = cap_override > 0 ? cap_override : (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
+  // a power-of-two capacity gives the regions a power-of-two stride (4 KiB of
+  // values at 256): measured on config 2, scatter +22 us and owner +12 us
+  // against 192 or 320 -- the 256 regions of a bin then share memory channels
+  if (cap_override <= 0 && (g.cap & (g.cap - 1)) == 0) g.cap += 64;
   const size_t nrec = bin_records(g.nbins, g.cap, n_rays);
   g.floats = nrec * 5 + (size_t)kBwdBlocks * (g.nbins + 16) + ovf_book_words(g.nbins, n_rays) + 4;
   return g;
