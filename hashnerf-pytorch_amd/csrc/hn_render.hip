@@ -2634,10 +2634,12 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   }();
   if (cap_override <= 0) cap_override = env_cap;
   g.cap = cap_override > 0 ? cap_override : (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
-  // a power-of-two capacity gives the regions a power-of-two stride (4 KiB of
-  // values at 256): measured on config 2, scatter +22 us and owner +12 us
-  // against 192 or 320 -- the 256 regions of a bin then share memory channels
-  if (cap_override <= 0 && (g.cap & (g.cap - 1)) == 0) g.cap += 64;
+  // an odd multiple of 64 records: the regions' stride (16 B x cap) then has
+  // as few factors of two as the 64-record granule allows.  Measured on
+  // config 2 (scatter / owner): 320 224 / 225 us, 448 227 / 226, 384 233 /
+  // 224, 256 247 / 237, 512 254 / 235 -- the 256 regions of a bin at a
+  // power-of-two stride share memory channels
+  if (cap_override <= 0 && ((g.cap >> 6) & 1) == 0) g.cap += 64;
   const size_t nrec = bin_records(g.nbins, g.cap, n_rays);
   g.floats = nrec * 5 + (size_t)kBwdBlocks * (g.nbins + 16) + ovf_book_words(g.nbins, n_rays) + 4;
   return g;
