@@ -1462,6 +1462,13 @@ HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], 
 #ifndef HN_SC_DIAG       // diagnostics (wrong gradients): 1 no record stores, 2 also no slot counters
 #define HN_SC_DIAG 0
 #endif
+// Coarse-pass feature grads, per ray: 64 samples x 32 features (+ HN_DC_PAD
+// floats, a per-ray stride off the power of two; workspace-internal)
+#ifndef HN_DC_PAD
+#define HN_DC_PAD 0
+#endif
+constexpr size_t kDcRay = (size_t)kSc * 32 + HN_DC_PAD;
+static_assert(HN_DC_PAD % 4 == 0, "f32x4 alignment");
 struct ScK {
   GridArgs g;
   int64_t B;
@@ -1558,7 +1565,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       }
     const int src = k.fine_src[ray * kSf + i];
     if (src < kSc) {                              // coarse twin: fine + coarse grads
-      const f32x4* tw = reinterpret_cast<const f32x4*>(k.dfeat_c + ((size_t)ray * (kSc / 32) + (src >> 5)) * 1024);
+      const f32x4* tw = reinterpret_cast<const f32x4*>(k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1772,7 +1779,7 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
   const int h = lane >> 5;
   const bool twin = src < kSc;
   const f32x4* dc =
-      reinterpret_cast<const f32x4*>(k.dfeat + ((size_t)ray * kSc + (twin ? src : 0)) * 32 + 16 * h);
+      reinterpret_cast<const f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)(twin ? src : 0) * 32 + 16 * h);
   f32x4 tw[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) tw[c] = twin ? dc[c] : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1933,13 +1940,13 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
       // coarse, split backward: the tile's feature grads in the saved-feature
       // tile order like the fine tiles (4 coalesced dwordx4 stores; the
       // per-point layout below took 16 scattered 4-B stores per lane and tile)
-      f32x4* dst = reinterpret_cast<f32x4*>(k.dfeat + ((size_t)ray * (kSc / 32) + tile0 + t) * 1024);
+      f32x4* dst = reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)(tile0 + t) * 1024);
 #pragma unroll
       for (int c = 0; c < 4; ++c) dst[64 * c + lane] = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
     } else {
       // coarse, fused backward: per-point feature grads [point][feature f][level]
       // for the fine units' ring hand-off (lane half h holds levels tile_level(m, h))
-      float* dst = k.dfeat + ((size_t)ray * kSc + qbase + p) * 32;
+      float* dst = k.dfeat + (size_t)ray * kDcRay + (size_t)(qbase + p) * 32;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         const int l = h ? tile_level(m, 1) : tile_level(m, 0);
@@ -2668,7 +2675,7 @@ struct WsLayout {
 static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
-  w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kSc * 32 + n * (kSc + kSf) * 4;
+  w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4;
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -2767,7 +2774,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* Pf = Pc + G_END;
   float* slab = Pf + G_END;
   float* dfeat = slab + (size_t)kBwdBlocks * kSlabSlots * W_END;
-  float* draw = dfeat + (size_t)a->n_rays * kSc * 32;
+  float* draw = dfeat + (size_t)a->n_rays * kDcRay;
   if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   B1K k;
   k.B = a->n_rays;
