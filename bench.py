@@ -51,12 +51,21 @@ PT_BYTES = 16 * 8 * 8          # one point: 16 levels x 8 corners x (2 x fp32)
 UNIQUE_PTS = 192               # per ray (the 64 coarse points recur in the fine pass)
 # per ray 192 unique points gathered + scatter-added, + 36 B ray I/O
 PATH_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2 + 36
-BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES * 2        # bwd kernel: re-gather + scatter-add
+# the backward launch's algorithmic bytes are the scatter-add half: it reads
+# the forward's saved features, it does not re-gather the table
+BWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # bwd launch: scatter-add
 FWD_BYTES_PER_RAY = UNIQUE_PTS * PT_BYTES            # fwd kernel: gather
+# SURVEY 8(d) FLOPs: NeRFSmall 18,688 FLOP per point forward, 37,376 backward;
+# 64 coarse + 192 fine evaluations per ray.  The backward kernel recomputes
+# the forward, so it carries both.
+MLP_FWD_FLOP_PER_RAY = 256 * 18688
+MLP_BWD_FLOP_PER_RAY = 256 * (18688 + 37376)
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+N_SIMDS = 1024                   # 256 CUs x 4 SIMDs
 # the kernels of one hn_render_bwd launch, per table-gradient scatter
 BWD_KERNELS = {"atomic": ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel"),
                "binned": ("render_comp_bwd_kernel", "render_bwd_kernel", "scatter_bins_kernel",
-                          "bin_reduce_kernel", "slab_reduce_kernel")}
+                          "ovf_place_kernel", "bin_reduce_kernel", "slab_reduce_kernel")}
 
 
 def measured_traffic(cfg_id, n_rand_override, scene, pretrain, scatter):
@@ -67,14 +76,28 @@ def measured_traffic(cfg_id, n_rand_override, scene, pretrain, scatter):
     them live; None when no file matches this workload."""
     path = os.path.join(ROOT, "profiles", f"traffic_config{cfg_id}_{scene}_p{pretrain}_{scatter}.json")
     if n_rand_override or not os.path.exists(path):
-        return None, None, None
+        return None, None, None, {}
     t = json.load(open(path))
     ks = t.get("kernels", {})
-    kern = BWD_KERNELS[scatter]
-    if not all(k in ks for k in kern):
-        return None, None, None
+    kern = [k for k in BWD_KERNELS[scatter] if k != "ovf_place_kernel" or k in ks]   # returns at once w/o spills
+    if not all(k in ks and "fetch_bytes" in ks[k] for k in kern):
+        return None, None, None, ks
     return (sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in kern), t.get("source"),
-            sum(ks[k].get("atomic_requests", 0.0) for k in kern) or None)
+            sum(ks[k].get("atomic_requests", 0.0) for k in kern) or None, ks)
+
+
+def mfma_busy(ks, kernel, source):
+    """MFMA-pipe busy fraction of one kernel from the same PMC file:
+    SQ_VALU_MFMA_BUSY_CYCLES (summed over all SIMDs; 32 cycles per
+    v_mfma_f32_32x32x16_bf16, 64 per v_mfma_f32_32x32x2_f32) over the SIMD
+    cycles of the dispatch, GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs;
+    MI355X_MICROARCH.md 'DVFS give-back') x 1024 SIMDs."""
+    e = ks.get(kernel, {})
+    busy, grbm = e.get("mfma_busy_cycles"), e.get("grbm_gui_active")
+    if not busy or not grbm:
+        return None
+    return {"busy_frac": round(busy / (N_SIMDS * grbm / 8.0), 4), "mfma_busy_cycles": busy,
+            "grbm_gui_active": grbm, "source": source}
 
 
 def cpu_baseline(cfg, seconds=12.0, n_rays=256):
@@ -130,9 +153,30 @@ def cpu_baseline(cfg, seconds=12.0, n_rays=256):
                       f"fwd+bwd+RAdam) on {threads} host threads, {dt:.1f} s"}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` (N > 1) outside torchrun: start torchrun with
+    N ranks on this node as a CHILD process (one process per GPU, this same
+    command line in each) and return its exit code.  Runs before anything
+    touches the GPU in this process (no torch.cuda call, no exec)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); N > 1 outside torchrun starts torchrun with N ranks")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=None, choices=sorted(CONFIGS))
@@ -153,7 +197,11 @@ def main():
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # same per-GPU workload at every N (weak scaling); --config 4 selects the
@@ -226,9 +274,11 @@ def main():
     value = world * B * args.steps / dt
     if rank == 0:
         scatter = "binned" if HF.L.lib().hn_render_scatter_mode(tr._cfg, B) == 2 else "atomic"
-        traffic, traffic_src, atomics = measured_traffic(cfg_id, args.n_rand, args.scene, args.pretrain, scatter)
+        traffic, traffic_src, atomics, pmc = measured_traffic(cfg_id, args.n_rand, args.scene, args.pretrain,
+                                                              scatter)
         bwd_gbs = B * BWD_BYTES_PER_RAY / (bwd_ms * 1e-3) / 1e9 if bwd_ms > 0 else 0.0
         fwd_gbs = B * FWD_BYTES_PER_RAY / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+        path_gbs = value / world * PATH_BYTES_PER_RAY / 1e9
         line = {
             "metric": "training rays/sec (fwd+bwd) on chair; PSNR@5k iters",
             "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
@@ -252,12 +302,29 @@ def main():
                          "traffic": round(traffic) if traffic else None,
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": B * BWD_BYTES_PER_RAY,
-                         "bytes_per_ray": BWD_BYTES_PER_RAY, "launch_ms": round(bwd_ms, 4),
-                         "scatter": scatter},
+                         "bytes_per_ray": BWD_BYTES_PER_RAY, "bytes_per_ray_meaning":
+                             "192 unique points x 16 levels x 8 corners x 8 B scatter-added",
+                         "launch_ms": round(bwd_ms, 4), "scatter": scatter,
+                         # the forward's gather and the whole step, same peak
+                         "fwd_gather": {"kernel": "render_fwd_kernel", "bytes_per_ray": FWD_BYTES_PER_RAY,
+                                        "launch_ms": round(fwd_ms, 4), "achieved": round(fwd_gbs, 1),
+                                        "frac": round(fwd_gbs / HBM_PEAK_GBS, 4)},
+                         "path": {"bytes_per_ray": PATH_BYTES_PER_RAY, "achieved": round(path_gbs, 1),
+                                  "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                                  "meaning": "gather + scatter-add + ray I/O per ray x rays/s (whole step)"}},
             "kernels": {"render_fwd_ms": round(fwd_ms, 4), "render_fwd_GBs": round(fwd_gbs, 1),
                         "render_bwd_ms": round(bwd_ms, 4),
-                        "path_GBs": round(value / world * PATH_BYTES_PER_RAY / 1e9, 1),
-                        "path_frac": round(value / world * PATH_BYTES_PER_RAY / 1e9 / HBM_PEAK_GBS, 4)},
+                        "path_GBs": round(path_gbs, 1), "path_frac": round(path_gbs / HBM_PEAK_GBS, 4)},
+            # MFMA: the NeRFSmall GEMMs of the forward (render_fwd_kernel) and of
+            # the MLP backward (render_bwd_kernel: forward recompute + backward)
+            "mfma": {"peak_TFLOPs": BF16_DENSE_PEAK_TFLOPS, "peak_meaning": "bf16 dense MFMA",
+                     "render_fwd_kernel": dict(
+                         alg_TFLOPs=round(B * MLP_FWD_FLOP_PER_RAY / (fwd_ms * 1e-3) / 1e12, 1) if fwd_ms > 0 else None,
+                         alg_frac=round(B * MLP_FWD_FLOP_PER_RAY / (fwd_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)
+                         if fwd_ms > 0 else None,
+                         pmc=mfma_busy(pmc, "render_fwd_kernel", traffic_src)),
+                     "render_bwd_kernel": dict(alg_flop_per_ray=MLP_BWD_FLOP_PER_RAY,
+                                               pmc=mfma_busy(pmc, "render_bwd_kernel", traffic_src))},
             "mlp_math": ("NeRFSmall GEMMs on v_mfma_f32_32x32x16_bf16 with f32 operands split into bf16 "
                          "parts: 3 parts in the forward (f32-accurate), 2 in the data/weight gradients"),
             "loss": round(float(loss.item()), 6),

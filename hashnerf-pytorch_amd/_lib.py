@@ -154,7 +154,8 @@ def check(status: int, what: str):
 
 
 FAULT_BITS = {1: "ring slot wait", 2: "ring drain (tiles left unscattered)", 4: "coarse-grad flag wait",
-              8: "dW buffer wait", 16: "binned-scatter overflow records exhausted"}
+              8: "dW buffer wait", 16: "binned-scatter overflow records exhausted",
+              32: "non-finite (NaN / Inf) feature gradient or sample point in the binned scatter"}
 
 
 def check_device_faults(clear: bool = True):
@@ -164,7 +165,7 @@ def check_device_faults(clear: bool = True):
     check(lib().hn_device_faults(C.byref(w), int(clear)), "device_faults")
     if w.value:
         what = ", ".join(v for k, v in FAULT_BITS.items() if w.value & k) or str(w.value)
-        raise RuntimeError(f"hashnerf_amd: the render backward reported a failed internal wait ({what}); "
+        raise RuntimeError(f"hashnerf_amd: the render backward reported a fault ({what}); "
                            "the gradients of the launches since the last check are invalid")
 
 

@@ -1307,7 +1307,12 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // clamps onto the box surface; the coarse levels of a T = 22 table) spills
 // but never runs out.  ovf_place_kernel buckets the spilled records by bin so
 // that each owner reads only its own.
-enum : int { kFaultBins = 16 };
+// kFaultNonFinite: a record input (feature grad or sample point) was NaN / Inf.
+// The fixed-point owner pass cannot carry such a value (the reference's
+// autograd would propagate it into embeddings[l].grad, hash_encoding.py:106),
+// so the gradient of that launch is flagged invalid instead of silently
+// dropping the contribution.
+enum : int { kFaultBins = 16, kFaultNonFinite = 32 };
 
 // Record r in memory.  HN_REC_AOS 0 (default): the values [nrec] f32x4 then
 // the words [nrec] u32.  HN_REC_AOS 1: groups of 4 records = 4 value quads
@@ -1579,6 +1584,13 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
             d = d + e[j];
           }
         }
+    }
+    {   // non-finite inputs (NaN / Inf in a grad or the point): one sum, one test per lane
+      float chk = (pt[0] + pt[1]) + pt[2];
+#pragma unroll
+      for (int l = 0; l < 16; ++l) chk += gf[0][l] + gf[1][l];
+      if (__ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
+        __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
@@ -2662,9 +2674,27 @@ static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   }
   if (!c) return kModeAtomic;
   const int want = c->scatter == 1 ? kModeAtomic : c->scatter == 2 ? kModeSplit : env;
-  (void)n_rays;
-  return want == kModeSplit && (16ll << c->grid.log2_hashmap_size) <= (long long)kScMaxBins << 13 ? kModeSplit
-                                                                                                : kModeAtomic;
+  const int T = c->grid.log2_hashmap_size;
+  if (want != kModeSplit || (16ll << T) > (long long)kScMaxBins << 13) return kModeAtomic;
+  // A record keeps its x1 corner's row as h(x0) ^ (2^nbits - 1), nbits =
+  // ctz(~x0) + 1 <= bit_length(x0) + 1 (4 bits of the entry word), and assumes
+  // both rows lie in one bin.  The cell index of a clamped point is at most
+  // (bmax - bmin) / grid_size, so that must fit the bin (or the level, when a
+  // bin holds whole levels: the xor is taken modulo 2^T).
+  const int shift = bin_geom(T, n_rays, c->bin_cap).shift;
+  if (shift < T) {
+    double cells = 0.0;
+    for (int l = 0; l < c->grid.n_levels; ++l)
+      for (int a = 0; a < 3; ++a) {
+        const double gs = c->grid.grid_size[l][a];
+        const double n = gs > 0.0 ? ((double)c->grid.box_max[a] - c->grid.box_min[a]) / gs : 1e30;
+        cells = n > cells ? n : cells;
+      }
+    int bits = 0;
+    while (bits < 40 && ldexp(1.0, bits) <= cells + 1.0) ++bits;   // bit_length of the largest cell index
+    if (bits + 1 > shift || bits + 1 > 15) return kModeAtomic;
+  }
+  return kModeSplit;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
 // coarse-pass feature grads [n][64][32] | d raw [n][256][4] | split: fine

@@ -73,7 +73,10 @@ const char* hn_status_string(int32_t status);
  * waves through bounded LDS waits; a wait that runs out (a protocol failure,
  * never expected) sets a bit here instead of hanging the GPU: 1 ring slot,
  * 2 ring drain (tiles left unscattered), 4 coarse-grad flag, 8 dW buffer,
- * 16 binned-scatter overflow records exhausted (gradient records lost).
+ * 16 binned-scatter overflow records exhausted (gradient records lost),
+ * 32 a NaN / Inf feature gradient or sample point reached the binned scatter
+ * (its exact fixed-point sums cannot carry it; the reference's autograd would
+ * propagate it into the table gradient).
  * Nonzero means the gradients of the launches since the last clear are
  * invalid.  This is the one entry point that synchronises (a blocking copy
  * from the device); call it at points where the host syncs anyway.

@@ -60,11 +60,19 @@ for k, cs in sorted(agg.items()):
 traffic = {"bench_args": bench_args, "source": f"pmc_{tag}", "kernels": {}}
 for k, cs in agg.items():
     f, w = cs.get("FETCH_SIZE"), cs.get("WRITE_SIZE")
+    ent = {}
     if f and w:
         ent = {"fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
         a = cs.get("TCC_EA0_ATOMIC_sum")
         if a:
             ent["atomic_requests"] = sum(a) / len(a)
+    # MFMA-pipe busy cycles (all SIMDs) and GRBM_GUI_ACTIVE (sum over the 8
+    # XCDs): bench.py's mfma busy fraction = busy / (1024 * grbm / 8)
+    for c, key in (("SQ_VALU_MFMA_BUSY_CYCLES", "mfma_busy_cycles"), ("GRBM_GUI_ACTIVE", "grbm_gui_active")):
+        v = cs.get(c)
+        if v:
+            ent[key] = sum(v) / len(v)
+    if ent:
         traffic["kernels"][k.replace("hn::", "")] = ent
 json.dump(traffic, open(f"{out}/traffic_{tag}.json", "w"), indent=1)
 EOF

@@ -1,0 +1,50 @@
+"""One rank of the device data-parallel test (tests/test_gpu_dp.py).
+
+Started by the test as a child process (RANK / WORLD_SIZE / MASTER_* in the
+environment), one per rank, all on cuda:0, torch.distributed over gloo.  The
+rank runs the HIP explicit-mode Trainer's forward + backward on ITS slice of a
+global batch the test drew (train.Trainer._fused_forward_backward, the step's
+launch sequence), all-reduces the gradients (Trainer.allreduce_grads: the
+SUM exchange of run_nerf.py:640-642 under SURVEY 8e's loss rule), and rank 0
+saves the reduced gradients.
+"""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(batch_path, out_path):
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    spec = torch.load(batch_path, weights_only=True)
+    dev = torch.device("cuda", 0)
+    data = SyntheticBlender(spec["H"], spec["W"], spec["n_img"], dev, seed=0)
+    args = default_args(**spec["args"])
+    tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)
+    tr.fuse_table_step = False
+    b = spec["ranks"][rank]
+    batch = dict(rays=b["rays"].to(dev), target=b["target"].to(dev), t_rand=b["t_rand"].to(dev),
+                 u=b["u"].to(dev), tv=(b["tv_cubes"], b["tv_mv"]) if "tv_mv" in b else None)
+    loss, _ = tr._fused_forward_backward(spec["i"], batch)
+    tr.allreduce_grads()
+    torch.cuda.synchronize()
+    from hashnerf_pytorch_amd import _lib
+    _lib.check_device_faults()
+    if rank == 0:
+        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+        torch.save({"table": tr.embed_fn.table.grad.cpu(), "mlp": [p.grad.cpu() for p in ws],
+                    "loss": loss.detach().cpu()}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

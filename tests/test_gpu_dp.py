@@ -1,0 +1,138 @@
+"""Data-parallel training step on the device (BASELINE configs[3]).
+
+* Two ranks (child processes, gloo, both on the one GPU) each run the HIP
+  explicit-mode Trainer on their half of a global batch and SUM-all-reduce
+  (Trainer.allreduce_grads).  The reduced table and NeRFSmall gradients must
+  equal the one-rank gradients of the whole batch (relative 1e-5: the two
+  ranks' binned table sums are each rounded once, the one-rank sum once; the
+  MLP weight-gradient slabs are summed in another order).  The exchange is
+  the one of run_nerf.py:640-642 (backward -> [all-reduce] -> step) under the
+  per-rank loss rule of train.dp_loss (MSE / world, entropy sums unscaled, TV
+  on rank 0 only).
+* The one-rank gradient itself is checked against the CPU oracle on a 32-ray
+  batch (the oracle's fine pass on the device's importance samples, as
+  test_gpu_parity.test_fused_step_vs_oracle_on_device_z), TV included.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _trainer(hn, n_rand, **over):
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    spec_args = dict(N_rand=n_rand, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=10 ** 6,
+                     sparse_loss_weight=1e-3)
+    spec_args.update(over)
+    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
+    tr = Trainer(default_args(**spec_args), data, DEV, seed=0)
+    tr.fuse_table_step = False
+    return tr, spec_args
+
+
+def _grads(tr):
+    ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+    return tr.embed_fn.table.grad.detach().cpu().clone(), [p.grad.detach().cpu().clone() for p in ws]
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def test_dp_two_ranks_equal_global_batch(hn, tmp_path):
+    tr, spec_args = _trainer(hn, 512)
+    i = 1
+    batch = tr.draw_batch(i)
+    assert batch["tv"] is not None
+    tr._fused_forward_backward(i, batch)
+    torch.cuda.synchronize()
+    g_table, g_mlp = _grads(tr)
+    world, B = 2, 512
+    ranks = []
+    for r in range(world):
+        sl = slice(r * B // world, (r + 1) * B // world)
+        d = {k: batch[k][sl].cpu() for k in ("rays", "target", "t_rand", "u")}
+        if r == 0:                                    # TV counted once (train.dp_loss)
+            d["tv_cubes"], d["tv_mv"] = list(batch["tv"][0]), batch["tv"][1].cpu()
+        ranks.append(d)
+    spec = dict(H=64, W=64, n_img=4, args=spec_args, i=i, ranks=ranks)
+    bpath, opath = str(tmp_path / "batch.pt"), str(tmp_path / "dp_out.pt")
+    torch.save(spec, bpath)
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dp_worker.py"), bpath, opath],
+                                      env=env, cwd=ROOT))
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=100))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert codes == [0] * world, codes
+    got = torch.load(opath, weights_only=True)
+    e = _rel(got["table"], g_table)
+    assert e <= 1e-5, f"table gradient: relative {e:.3e}"
+    for k, (a, b) in enumerate(zip(got["mlp"], g_mlp)):
+        e = _rel(a, b)
+        assert e <= 1e-5, f"MLP gradient {k}: relative {e:.3e}"
+
+
+def test_trainer_one_rank_gradient_vs_oracle(hn, oracle):
+    """The explicit trainer's launch sequence (sampler batch, fused render,
+    TV, fused loss, binned backward + TV backward) on 32 rays against the
+    oracle's autograd of run_nerf.py:612-636 with the same inputs."""
+    from hashnerf_pytorch_amd import functional as HF
+    O = oracle
+    tr, _ = _trainer(hn, 32)
+    e = tr.embed_fn
+    tab0 = e.table.detach().cpu().clone()
+    nets = (tr.kw_train["network_fn"], tr.kw_train["network_fine"])
+    w0 = [[p.detach().cpu().clone() for p in n.weights()] for n in nets]
+    batch = tr.draw_batch(1)
+    HF.DEBUG_KEEP = True
+    try:
+        tr._fused_forward_backward(1, batch)
+    finally:
+        HF.DEBUG_KEEP = False
+    z_fine = HF.LAST["z_fine"].cpu()
+    g_table, g_mlp = _grads(tr)
+    box = tuple(torch.as_tensor(v, dtype=torch.float32).cpu() for v in tr.data.bounding_box)
+    tab = tab0.clone().requires_grad_(True)
+    wc = {k: v.clone().requires_grad_(True) for k, v in zip(O.MLP_KEYS, w0[0])}
+    wf = {k: v.clone().requires_grad_(True) for k, v in zip(O.MLP_KEYS, w0[1])}
+    T = int(e.log2_hashmap_size)
+    ret = O.render_rays(batch["rays"].cpu(), wc, wf, tab, box[0], box[1], O.level_resolutions(16, 16, 512), T,
+                        t_rand=batch["t_rand"].cpu(), u=batch["u"].cpu(), white_bkgd=True, z_fine=z_fine)
+    same = np.isclose(z_fine.numpy(), ret["z_vals"].detach().numpy(), rtol=0, atol=1e-5)
+    assert same.mean() > 0.97, f"only {same.mean():.4f} of fine samples agree"
+    cubes, mv = batch["tv"]
+    tv = sum(O.total_variation_loss(tab[l], l, mv[l].cpu(), T) for l in range(16))
+    loss = O.training_loss(ret, batch["target"].cpu(), 1e-3) + 1e-4 * tv
+    loss.backward()
+    err = _rel(g_table, tab.grad)
+    assert err <= 5e-4, f"table gradient: relative {err:.3e}"
+    for k, (a, ref) in enumerate(zip(g_mlp, [wc[k].grad for k in O.MLP_KEYS] + [wf[k].grad for k in O.MLP_KEYS])):
+        err = _rel(a, ref)
+        assert err <= 5e-4, f"MLP gradient {k}: relative {err:.3e}"

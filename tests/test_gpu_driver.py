@@ -183,6 +183,37 @@ def test_trainer_step_index_follows_reference_loop(hn):
     assert default_args().tv_until == 1001            # run_nerf.py:636-638: TV through i = 1001
 
 
+def test_trainer_fused_table_step_bitwise(hn):
+    """the trainer path that fuses the table's RAdam step into the
+    binned owner pass (take_step -> render_bwd(table_step) -> step() of the
+    MLP groups only) against the unfused path (gradient stored, hn_radam_step)
+    from the same seed: table, moments and step counters bitwise equal after
+    8 steps (the update starts at step 6, N_sma >= 5).  No TV term, so the
+    fused branch is the one taken."""
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
+    res = {}
+    for fuse in (True, False):
+        args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=0.0, sparse_loss_weight=1e-3)
+        tr = Trainer(args, data, DEV, seed=3)
+        tr.fuse_table_step = fuse
+        torch.manual_seed(11)
+        for _ in range(8):
+            tr.step()
+        t = tr.embed_fn.table
+        st = tr.optimizer.state[t]
+        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+        res[fuse] = (t.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(), st["step"],
+                     [p.detach().clone() for p in ws], [tr.optimizer.state[p]["step"] for p in ws])
+    a, b = res[True], res[False]
+    for k in range(3):
+        assert torch.equal(a[k], b[k]), k
+    assert a[3] == b[3] == 8
+    for x, y in zip(a[4], b[4]):
+        assert torch.equal(x, y)
+    assert a[5] == b[5] == [8] * 10
+
+
 @pytest.mark.gpu
 def test_device_fault_word_clear_after_fused_steps(hn):
     """The render backward's bounded waits never run out in a normal step:

@@ -209,3 +209,27 @@ def test_fused_table_step_bitwise(hn, mode):
     assert torch.equal(pf, pr)
     if mode:
         assert not torch.equal(pf, p0)
+
+
+def test_nonfinite_gradient_raises_fault(hn):
+    """A NaN upstream gradient on one ray: the reference's autograd carries it
+    into embeddings[l].grad (hash_encoding.py:106); the binned owner pass's
+    fixed-point sums cannot, so the scatter sets the sticky fault bit 32 and
+    check_device_faults raises.  Clean inputs leave the
+    word clear."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 512, 14, 21, "binned")
+    _bwd(HF, emb, ws, st, grads)                      # clean: no fault (checked inside)
+    bad = dict(grads)
+    g = bad["g_rgb"].clone()
+    g[7, 1] = float("nan")
+    bad["g_rgb"] = g
+    d_table = torch.zeros_like(emb.table)
+    keep, HF.CHECK_FAULTS = HF.CHECK_FAULTS, False     # read the word here, not inside render_bwd
+    try:
+        HF.render_bwd(st, bad, d_table, HF.zeros_like_all(ws))
+    finally:
+        HF.CHECK_FAULTS = keep
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="non-finite"):
+        HF.L.check_device_faults()
+    HF.L.check_device_faults()                        # cleared by the raising read
