@@ -40,10 +40,13 @@ CONFIGS = {
     # scannet_scene0000.txt: white_bkgd False; the bbox is the mesh bounds
     # (load/load_scannet.py:105), far tighter than the sample range, so most
     # samples are out of the box (extrapolated weights, SURVEY trap 3)
+    # use_batching (no_batching False, configs/scannet_scene0000.txt:6): the
+    # global shuffled pool of every training ray (run_nerf.py:505-521, 544-555)
     5: dict(workload="scannet-style unbounded scene: bbox +-1 inside the 2..6 sample range, black bkgd, "
-                     "sparse_loss_weight 1e-3, N_rand=4096 per GPU, 64+128 (BASELINE configs[4])",
+                     "sparse_loss_weight 1e-3, use_batching ray pool, N_rand=4096 per GPU, 64+128 "
+                     "(BASELINE configs[4])",
             N_rand=4096, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6,
-            white_bkgd=False, sparse_loss_weight=1e-3, bbox=((-1., -1., -1.), (1., 1., 1.))),
+            white_bkgd=False, sparse_loss_weight=1e-3, bbox=((-1., -1., -1.), (1., 1., 1.)), no_batching=False),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 ATOMIC_PEAK_GREQ = round(1.3e12 / 64 / 1e9, 1)   # float atomics: 1.3 TB/s of 64-B requests
@@ -228,7 +231,8 @@ def main():
     targs = default_args(N_rand=cfg["N_rand"], log2_hashmap_size=cfg["log2_hashmap_size"],
                          finest_res=cfg["finest_res"], tv_loss_weight=cfg["tv_loss_weight"],
                          tv_until=cfg.get("tv_until", 1001), white_bkgd=cfg.get("white_bkgd", True),
-                         sparse_loss_weight=cfg.get("sparse_loss_weight", 1e-10))
+                         sparse_loss_weight=cfg.get("sparse_loss_weight", 1e-10),
+                         no_batching=cfg.get("no_batching", True))
     t_data = time.perf_counter()
     data = SyntheticBlender(400, 400, 100, dev, seed=0, scene=args.scene)
     t_data = time.perf_counter() - t_data

@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 8                 # HN_ABI_VERSION
+ABI_VERSION = 9                 # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -90,6 +90,11 @@ class HnRaySampler(C.Structure):
                 ("seed", C.c_uint64)]
 
 
+class HnRayPool(C.Structure):
+    _fields_ = [("n_images", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("pose_stride", C.c_int32),
+                ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+                ("near", C.c_float), ("far", C.c_float), ("seed", C.c_uint64)]
+
 
 # name -> (restype, argtypes); must match include/hashnerf_amd.h exactly.
 SIGNATURES = {
@@ -115,6 +120,8 @@ SIGNATURES = {
     "hn_sample_rays_morton_workspace_bytes": (C.c_size_t, [C.POINTER(HnRaySampler)]),
     "hn_sample_rays_morton": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P, C.c_size_t,
                                           _P]),
+    "hn_sample_pool": (C.c_int32, [C.POINTER(HnRayPool), _P, _P, _P, C.c_int64, C.c_int64, _P, _P, _P]),
+    "hn_blender_images": (C.c_int32, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P]),
     "hn_loss_fwd": (C.c_int32, [_P, _P, _P, _P, _P, C.c_int64, _P, C.c_int32, C.c_float, C.c_float,
                                 C.c_float, _P, _P]),
     "hn_loss_bwd": (C.c_int32, [_P, _P, _P, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_float, _P,

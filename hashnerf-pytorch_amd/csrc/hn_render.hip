@@ -2161,7 +2161,15 @@ void render_bwd_kernel(B1K k) {
     }
     // split: wave 0 has the block's 2 * n_rays coarse tiles, waves 1-3 share
     // its 6 * n_rays fine tiles (balanced); fused: wave 0 joins waves 1-2
-    if (!SPLIT || wave != 0) {
+    if (SPLIT && wave != 0) {
+      // split: wave w owns part w - 1 (tiles 2(w-1), 2(w-1)+1) of every ray of
+      // the block, in ray order -- a static split (the units are equal), so each
+      // dW slab, and with the fixed-order slab reduce the MLP gradients, are
+      // bitwise reproducible
+      wring_prime(wr, k.Pf, lane);
+      for (int i = 0; i < n_rays; ++i)
+        b1_unit<kSf, MODE>(k, block_ray(i), wave - 1, X, dw, wr, &ring, pc, &sync[0], i + 1);
+    } else if (!SPLIT) {
       wring_prime(wr, k.Pf, lane);
       for (;;) {
         int u = 0;

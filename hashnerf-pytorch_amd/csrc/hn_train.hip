@@ -145,6 +145,101 @@ __global__ __launch_bounds__(kMortonThreads) void morton_emit_kernel(hn_ray_samp
 }
 
 // ---------------------------------------------------------------------------
+// use_batching ray pool (run_nerf.py:505-521, 544-555).  The reference
+// materialises rays_rgb = [every training pixel][ro, rd, rgb] (rays from
+// get_rays_np, ray_util.py:82-93: float64 arithmetic under numpy 2, then
+// .astype(float32)), shuffles it once and again after every epoch, and takes
+// consecutive N_rand slices.  Here the shuffle is a keyed bijection of the
+// pool index (cycle-walked Feistel, as the per-image sampler), so nothing is
+// materialised: pool position q -> pixel perm(q) = (image, row, column) ->
+// its ray, computed in float64 and rounded once, and its target colour.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sample_pool_kernel(hn_ray_pool p, const float* __restrict__ images,
+                                                          const float* __restrict__ poses,
+                                                          const int32_t* __restrict__ ids, int64_t start, int64_t n,
+                                                          int half, float* __restrict__ rays,
+                                                          float* __restrict__ target) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t hw = (uint32_t)p.H * (uint32_t)p.W;
+  const uint32_t N = (uint32_t)p.n_images * hw;
+  uint32_t x = (uint32_t)(start + i);
+  do {
+    x = feistel(x, half, p.seed);
+  } while (x >= N);
+  const int img = ids[x / hw];
+  const uint32_t pix = x % hw;
+  const int py = (int)(pix / (uint32_t)p.W), px = (int)(pix % (uint32_t)p.W);
+  const float* c = poses + (size_t)img * p.pose_stride;
+  // dirs = [(i - K[0][2]) / K[0][0], -(j - K[1][2]) / K[1][1], -1] (float64: K is)
+  const double d0 = ((double)px - p.cx) / p.fx;
+  const double d1 = -((double)py - p.cy) / p.fy;
+  const double d2 = -1.0;
+  float* out = rays + 11 * i;
+  float d[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {   // np.sum(dirs[..., None, :] * c2w[:3, :3], -1): ((p0 + p1) + p2)
+    d[a] = (float)((d0 * (double)c[4 * a] + d1 * (double)c[4 * a + 1]) + d2 * (double)c[4 * a + 2]);
+    out[a] = c[4 * a + 3];
+    out[3 + a] = d[a];
+  }
+  out[6] = p.near;
+  out[7] = p.far;
+  const float nrm = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);   // render(): viewdirs (:350)
+#pragma unroll
+  for (int a = 0; a < 3; ++a) out[8 + a] = d[a] / nrm;
+  const float* px3 = images + 3 * (((size_t)img * p.H + py) * p.W + px);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) target[3 * i + a] = px3[a];
+}
+
+// ---------------------------------------------------------------------------
+// Blender image preparation: load/load_blender.py:63 (uint8 PNG / 255. in
+// float64, .astype(float32)), :78-86 (half_res: cv2.resize INTER_AREA to H/2 x
+// W/2, stored into a float64 array) and run_nerf.py:259-262 (white_bkgd:
+// rgb * a + (1 - a), float32 arithmetic at full resolution, float64 after
+// half_res; the trainer's torch.Tensor rounds to float32).  INTER_AREA at an
+// exact factor 2 is the 2 x 2 box mean; OpenCV's float path sums
+// ((top-left + top-right) + (bottom-left + bottom-right)) * 0.25 (cv2 is not in
+// the image: that order is restated).  One thread per output pixel.
+// ---------------------------------------------------------------------------
+HN_DEV float u8_unit(uint8_t v) { return (float)((double)v / 255.0); }
+
+__global__ __launch_bounds__(256) void blender_images_kernel(const uint8_t* __restrict__ rgba, int64_t n_px, int H,
+                                                             int W, int half, int mode, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_px) return;
+  const int Ho = half ? H / 2 : H, Wo = half ? W / 2 : W;
+  const int64_t img = t / ((int64_t)Ho * Wo);
+  const int r = (int)(t / Wo % Ho), col = (int)(t % Wo);
+  float v[4];
+  if (!half) {
+    const uint8_t* s = rgba + 4 * ((img * H + r) * (int64_t)W + col);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = u8_unit(s[c]);
+  } else {
+    const uint8_t* s0 = rgba + 4 * ((img * H + 2 * r) * (int64_t)W + 2 * col);
+    const uint8_t* s1 = s0 + 4 * (int64_t)W;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      v[c] = ((u8_unit(s0[c]) + u8_unit(s0[4 + c])) + (u8_unit(s1[c]) + u8_unit(s1[4 + c]))) * 0.25f;
+  }
+  if (mode == 0) {   // RGBA as load_blender_data returns it
+#pragma unroll
+    for (int c = 0; c < 4; ++c) out[4 * t + c] = v[c];
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float o = v[c];
+    if (mode == 1) {
+      o = half ? (float)((double)v[c] * (double)v[3] + (1.0 - (double)v[3])) : v[c] * v[3] + (1.f - v[3]);
+    }
+    out[3 * t + c] = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Loss.  Forward: one workgroup, fp64 accumulation of the reductions (the
 // value is reported, its gradient does not depend on the summation order).
 // ---------------------------------------------------------------------------
@@ -369,5 +464,35 @@ extern "C" int32_t hn_loss_fwd_bwd(const float* rgb, const float* rgb0, const fl
   hipLaunchKernelGGL(loss_fwd_bwd_kernel, dim3(blocks), dim3(kLossThreads), 0, (hipStream_t)stream, rgb, rgb0,
                      target, sp, sp0, n_rays, tv, n_tv, world, sparse_w, tv_w, out, g_loss, g_rgb, g_rgb0, g_sp,
                      g_sp0, g_tv);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_sample_pool(const hn_ray_pool* p, const float* images, const float* poses,
+                                  const int32_t* image_ids, int64_t start, int64_t n_rays, float* rays, float* target,
+                                  void* stream) {
+  if (!p) return HN_E_NULL;
+  if (n_rays < 0 || start < 0) return HN_E_SHAPE;
+  if (n_rays == 0) return HN_OK;
+  if (!images || !poses || !image_ids || !rays || !target) return HN_E_NULL;
+  if (p->n_images <= 0 || p->H <= 0 || p->W <= 0 || p->pose_stride < 12) return HN_E_SHAPE;
+  const uint64_t N = (uint64_t)p->n_images * (uint64_t)p->H * (uint64_t)p->W;
+  if (N > (1ull << 30) || (uint64_t)start + (uint64_t)n_rays > N) return HN_E_SHAPE;   // one epoch's positions
+  int bits = 2;
+  while ((1ull << bits) < N) bits += 2;
+  const unsigned blocks = (unsigned)((n_rays + 255) / 256);
+  hipLaunchKernelGGL(sample_pool_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p, images, poses,
+                     image_ids, start, n_rays, bits / 2, rays, target);
+  return hip_status(hipGetLastError());
+}
+
+extern "C" int32_t hn_blender_images(const uint8_t* rgba, int64_t n_images, int32_t H, int32_t W, int32_t half_res,
+                                     int32_t mode, float* out, void* stream) {
+  if (n_images < 0 || H <= 0 || W <= 0 || mode < 0 || mode > 2) return HN_E_SHAPE;
+  if (half_res && ((H | W) & 1)) return HN_E_SHAPE;   // INTER_AREA at exactly half
+  if (n_images == 0) return HN_OK;
+  if (!rgba || !out) return HN_E_NULL;
+  const int64_t n_px = n_images * (int64_t)(half_res ? H / 2 : H) * (half_res ? W / 2 : W);
+  hipLaunchKernelGGL(blender_images_kernel, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     rgba, n_px, H, W, half_res ? 1 : 0, mode, out);
   return hip_status(hipGetLastError());
 }

@@ -391,6 +391,49 @@ def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1):
     return rays, target
 
 
+def sample_pool(images, poses, image_ids, K, near, far, seed, start, n_rays):
+    """use_batching draw (run_nerf.py:505-521, 544-555): pool positions
+    [start, start + n_rays) of the epoch whose shuffle key is `seed`, as the
+    [n, 11] ray batch and [n, 3] targets (hn_sample_pool).  images [N, H, W, 3]
+    and poses [N, 3|4, 4] on the device; image_ids the training image indices
+    (device int32); K the 3x3 intrinsics (host numbers, used in float64)."""
+    L.require_device(images, poses)
+    images, poses = images.contiguous(), poses.contiguous()
+    if image_ids.dtype != torch.int32 or not image_ids.is_cuda:
+        raise TypeError("hashnerf_amd.sample_pool: image_ids must be a device int32 tensor")
+    p = L.HnRayPool()
+    p.n_images = int(image_ids.numel())
+    p.H, p.W = int(images.shape[1]), int(images.shape[2])
+    p.pose_stride = int(poses.shape[1] * poses.shape[2])
+    p.fx, p.fy, p.cx, p.cy = float(K[0][0]), float(K[1][1]), float(K[0][2]), float(K[1][2])
+    p.near, p.far = float(near), float(far)
+    p.seed = int(seed) & ((1 << 64) - 1)
+    dev = images.device
+    rays = torch.empty((n_rays, 11), dtype=torch.float32, device=dev)
+    target = torch.empty((n_rays, 3), dtype=torch.float32, device=dev)
+    L.check(L.lib().hn_sample_pool(p, L.ptr(images), L.ptr(poses), L.ptr(image_ids.contiguous()), int(start),
+                                   int(n_rays), L.ptr(rays), L.ptr(target), L.stream(dev)), "sample_pool")
+    return rays, target
+
+
+BLENDER_MODES = {"rgba": 0, "white": 1, "rgb": 2}
+
+
+def blender_images(rgba_u8, half_res=False, mode="rgba"):
+    """hn_blender_images: uint8 RGBA [n, H, W, 4] on the device -> float32
+    images as load/load_blender.py:63-86 (/ 255., half_res INTER_AREA) and,
+    mode="white" / "rgb", run_nerf.py:259-262's composite / channel cut."""
+    if not rgba_u8.is_cuda or rgba_u8.dtype != torch.uint8 or rgba_u8.dim() != 4 or rgba_u8.shape[-1] != 4:
+        raise TypeError("hashnerf_amd.blender_images: expects a device uint8 tensor [n, H, W, 4]")
+    n, H, W, _ = rgba_u8.shape
+    Ho, Wo = (H // 2, W // 2) if half_res else (H, W)
+    m = BLENDER_MODES[mode]
+    out = torch.empty((n, Ho, Wo, 4 if m == 0 else 3), dtype=torch.float32, device=rgba_u8.device)
+    L.check(L.lib().hn_blender_images(L.ptr(rgba_u8.contiguous()), n, H, W, int(bool(half_res)), m, L.ptr(out),
+                                      L.stream(rgba_u8.device)), "blender_images")
+    return out
+
+
 _SAMPLER_WS = {}
 
 

@@ -1,8 +1,10 @@
-"""Training-step driver: the no_batching loop of run_nerf.py:541-651 with
-on-device ray sampling, plus data-parallel gradient exchange.
+"""Training-step driver: the loop of run_nerf.py:541-651 with on-device ray
+sampling, plus data-parallel gradient exchange.
 
 One step = draw one training image per rank, N_rand pixels without
-replacement (centre crop for the first ``precrop_iters``), render with the
+replacement (centre crop for the first ``precrop_iters``) -- or, with
+use_batching (no_batching False, run_nerf.py:505-521, 544-555), the next
+N_rand positions of the shuffled pool of every training ray -- render with the
 fused kernels, loss (MSE fine + coarse + sparse_loss_weight * entropy sums
 + tv_loss_weight * TV), backward, gradient all-reduce (DP), RAdam step and
 the exponential lr decay of run_nerf.py:647-651 (applied after step() with
@@ -116,7 +118,7 @@ def default_args(**over):
              precrop_frac=0.5, finest_res=512, log2_hashmap_size=19, sparse_loss_weight=1e-10,
              tv_loss_weight=1e-6, netchunk=1024 * 64, chunk=1024 * 32, dataset_type="blender",
              i_embed=1, i_embed_views=2, no_reload=True, ft_path=None, basedir=None, expname=None,
-             H=400, W=400, n_train=100, lindisp=False, no_ndc=False, tv_until=1001)
+             H=400, W=400, n_train=100, lindisp=False, no_ndc=False, tv_until=1001, no_batching=True)
     a.update(over)
     return types.SimpleNamespace(**a)
 
@@ -265,6 +267,17 @@ class Trainer:
         self.coords_crop = torch.stack([cj, ci], -1).reshape(-1, 2)
         self.crop = (H // 2 - dH, W // 2 - dW, 2 * dH, 2 * dW)
         self._grads = None
+        # use_batching (no_batching False, e.g. configs/scannet_scene0000.txt:6):
+        # the global shuffled ray pool of run_nerf.py:505-521 over the training
+        # images, consumed N_rand positions per step and reshuffled per epoch
+        # (hn_sample_pool: the shuffle is a keyed bijection, nothing materialised)
+        self.use_batching = not getattr(args, "no_batching", True)
+        self.i_batch, self.epoch = 0, 0
+        if self.use_batching and mode == "eager":
+            raise NotImplementedError("Trainer(mode='eager') draws per-image batches only (no_batching)")
+        if self.use_batching:
+            self._pool_ids = torch.as_tensor(data.i_train).to(device=self.device, dtype=torch.int32)
+            self._pool_n = int(self._pool_ids.numel()) * H * W
         # the render backward's sticky fault word (hn_device_faults) is read
         # every this many steps: one blocking copy, so a failed internal wait
         # can never leave silently wrong gradients behind for long
@@ -273,10 +286,47 @@ class Trainer:
         # backward's owner pass when the step has no TV term
         self.fuse_table_step = True
 
+    def _train_image(self):
+        """np.random.choice(i_train) (run_nerf.py:578) from the host generator."""
+        d = self.data
+        return int(d.i_train[int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))])
+
+    def _pool_draw(self):
+        """The next use_batching batch (run_nerf.py:544-555): pool positions
+        [i_batch, i_batch + N_rand) of this epoch's shuffle -- with world > 1
+        the global batch of world * N_rand positions, rank r taking its share --
+        then i_batch advances and wraps (new epoch, new shuffle key) once the
+        pool is used up.  The last batch of an epoch is short, as the
+        reference's slice."""
+        a, d = self.args, self.data
+        gB = a.N_rand * self.world
+        rem = min(gB, self._pool_n - self.i_batch)
+        lo = self.i_batch + rem * self.rank // self.world
+        hi = self.i_batch + rem * (self.rank + 1) // self.world
+        rays, target = HF.sample_pool(d.images, d.poses, self._pool_ids, d.K, 2., 6.,
+                                      _step_seed(self.seed, 0, -1 - self.epoch), lo, hi - lo)
+        self.i_batch += gB
+        if self.i_batch >= self._pool_n:
+            self.epoch += 1
+            self.i_batch = 0
+        return rays, target
+
+    def _draw_rays(self, i: int):
+        """The step's rays and targets: the shuffled pool (use_batching) or
+        N_rand pixels of one training image (device sampler, centre crop
+        before precrop_iters)."""
+        if self.use_batching:
+            return self._pool_draw()
+        a, d = self.args, self.data
+        img_i = self._train_image()
+        crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
+        return HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
+                              _step_seed(self.seed, self.rank, i), order=self.ray_order)
+
     def sample_rays(self, i: int):
         """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
         d, a = self.data, self.args
-        img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
+        img_i = self._train_image()
         coords = self.coords_crop if i < a.precrop_iters else self.coords_full
         sel = torch.randperm(coords.shape[0], device=self.device, generator=self.gen)[: a.N_rand]
         c = coords[sel]
@@ -335,11 +385,8 @@ class Trainer:
         Returns a dict rays [B, 11], target [B, 3], t_rand, u, tv (or None)."""
         a, d, kw = self.args, self.data, self.kw_train
         i = self.global_step + 1 if i is None else i
-        B = a.N_rand
-        img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
-        crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
-        rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], B, d.K, 2., 6., crop,
-                                      _step_seed(self.seed, self.rank, i), order=self.ray_order)
+        rays, target = self._draw_rays(i)
+        B = rays.shape[0]
         perturb = kw.get("perturb", 0.) > 0.
         # two draws in render_rays' order (run_nerf_helpers.py:528, then :276 via :548): the
         # autograd and reference-path modes draw them the same way, so all
@@ -413,12 +460,8 @@ class Trainer:
         else:
             self.optimizer.zero_grad(set_to_none=True)
             if self.mode == "autograd":
-                d = self.data
-                img_i = int(torch.randint(len(d.i_train), (1,), generator=self.cpu_gen))
-                crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
-                rays, target = HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
-                                              _step_seed(self.seed, self.rank, i), order=self.ray_order)
-                rgb, depth, acc, extras = render_ray_batch(rays, (a.N_rand,), chunk=a.chunk, retraw=True,
+                rays, target = self._draw_rays(i)
+                rgb, depth, acc, extras = render_ray_batch(rays, (rays.shape[0],), chunk=a.chunk, retraw=True,
                                                            **self.kw_train)
                 tv = None
                 if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 8
+#define HN_ABI_VERSION 9
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -267,6 +267,42 @@ int32_t hn_sample_rays(const hn_ray_sampler* s, const float* image, const float*
 size_t hn_sample_rays_morton_workspace_bytes(const hn_ray_sampler* s);
 int32_t hn_sample_rays_morton(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
                               float* rays, float* target, void* workspace, size_t ws_bytes, void* stream);
+
+/* use_batching ray pool (run_nerf.py:505-521 builds rays_rgb from every training
+ * pixel and shuffles it; :544-555 takes consecutive N_rand slices and reshuffles
+ * after each epoch).  The pool is never materialised: position q of an epoch
+ * maps to pool pixel perm(q) (a keyed, cycle-walked Feistel bijection of
+ * [0, n_images * H * W), the epoch's shuffle; pool order is (image, row,
+ * column) as rays_rgb's reshape), whose ray is get_rays_np's (ray_util.py:82-93:
+ * float64 arithmetic, rounded to float32 as rays_rgb.astype(np.float32)) and
+ * whose target is the image pixel.  Batch k of an epoch = positions
+ * [k N_rand, min((k + 1) N_rand, pool size)): the caller passes start = k N_rand
+ * and the batch length (the last batch of an epoch is short, as the
+ * reference's slice).  rays[n][11] and target[n][3] as hn_sample_rays. */
+typedef struct hn_ray_pool {
+  int32_t n_images;       /* training images in the pool (image_ids[n_images]) */
+  int32_t H, W;
+  int32_t pose_stride;    /* floats between consecutive c2w matrices in `poses` (12 or 16) */
+  double fx, fy, cx, cy;  /* intrinsics K, float64 as get_rays_np uses them */
+  float near, far;
+  uint64_t seed;          /* the epoch's shuffle key */
+} hn_ray_pool;
+/* images: device [n_all][H][W][3]; poses: device [n_all][.][4] (row-major
+ * c2w, pose_stride floats apart); image_ids: device int32 [n_images] (i_train). */
+int32_t hn_sample_pool(const hn_ray_pool* p, const float* images, const float* poses, const int32_t* image_ids,
+                       int64_t start, int64_t n_rays, float* rays, float* target, void* stream);
+
+/* Blender image preparation (load/load_blender.py:63, :78-86; run_nerf.py:259-262):
+ * rgba: device uint8 [n][H][W][4] (the PNGs) -> out, float32:
+ *   x = float32(u8 / 255.0)  (float64 division, as np.array(imgs) / 255.);
+ *   half_res: 2 x 2 box mean (cv2.resize INTER_AREA to H/2 x W/2; H, W even);
+ *   mode 0: RGBA [n][H'][W'][4] (what load_blender_data returns);
+ *   mode 1: white background, rgb * a + (1 - a) -> [n][H'][W'][3] (float32
+ *           arithmetic at full resolution, float64 after half_res as the
+ *           reference's float64 half-res array, rounded to float32);
+ *   mode 2: rgb only -> [n][H'][W'][3] (white_bkgd False). */
+int32_t hn_blender_images(const uint8_t* rgba, int64_t n_images, int32_t H, int32_t W, int32_t half_res,
+                          int32_t mode, float* out, void* stream);
 
 /* Training loss (run_nerf.py:612-636 with the data-parallel rule of
  * SURVEY 8e): loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * (sum sp + sum sp0)

@@ -382,6 +382,47 @@ def gen_radam(ref):
     save("radam", p0=p0, t0=t0, ga=np.stack(ga), gb=np.stack(gb), pa=np.stack(pas), pb=np.stack(pbs))
 
 
+def gen_pool_rays(ref):
+    """use_batching's ray pool (run_nerf.py:509-515): get_rays_np (the
+    reference's ray_util.py:82-93, called here) of every training image, the
+    rays_rgb stacking / transposition / reshape / float32 cast of those lines
+    restated with the same numpy calls (run_nerf.py imports configargparse /
+    imageio, absent here).  3 training images of 20 x 24 among 5 (i_train =
+    0, 2, 3), cameras as make_golden.cameras, K in float64 as load_blender."""
+    H, W = 20, 24
+    focal = .5 * W / np.tan(.5 * CAM_ANGLE_X)
+    K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])
+    poses = np.stack([c.numpy() for c in cameras(5)]).astype(np.float32)
+    images = rng(31).random((5, H, W, 3), dtype=np.float32)
+    i_train = np.array([0, 2, 3])
+    rays = np.stack([ref.ray_util.get_rays_np(H, W, K, p) for p in poses[:, :3, :4]], 0)
+    rays_rgb = np.concatenate([rays, images[:, None]], 1)
+    rays_rgb = np.transpose(rays_rgb, [0, 2, 3, 1, 4])
+    rays_rgb = np.stack([rays_rgb[i] for i in i_train], 0)
+    rays_rgb = np.reshape(rays_rgb, [-1, 3, 3]).astype(np.float32)
+    save("pool_rays", H=H, W=W, K=K, poses=poses, images=images, i_train=i_train, rays_rgb=rays_rgb)
+
+
+def gen_blender_images(ref):
+    """Blender image preparation on a synthetic RGBA array (no PNGs needed):
+    load/load_blender.py:63 `(np.array(imgs) / 255.).astype(np.float32)`, and
+    run_nerf.py:259-262 `images[..., :3] * images[..., -1:] + (1. - images[...,
+    -1:])` at full resolution, with the reference's own numpy expressions.
+    half_res (:78-86) calls cv2.resize(INTER_AREA), and cv2 is not in the
+    image: the fixture holds the exact (float64) 2 x 2 means of the float32
+    pixels instead, and the float64 composite of those means; a float32
+    INTER_AREA sum is within 1 ulp of them (tests/test_blender_data.py)."""
+    g = rng(37)
+    rgba = g.integers(0, 256, size=(3, 6, 8, 4), dtype=np.uint8)
+    rgba[0, 0, 0] = (255, 0, 0, 0)          # fully transparent
+    rgba[0, 0, 1] = (10, 20, 30, 255)       # opaque
+    imgs = (np.array(rgba) / 255.).astype(np.float32)
+    white = imgs[..., :3] * imgs[..., -1:] + (1. - imgs[..., -1:])
+    f = imgs.astype(np.float64)
+    half_mean = 0.25 * (f[:, 0::2, 0::2] + f[:, 0::2, 1::2] + f[:, 1::2, 0::2] + f[:, 1::2, 1::2])
+    save("blender_images", rgba=rgba, imgs=imgs, white=white, half_mean=half_mean)
+
+
 def main():
     torch.set_num_threads(8)
     ref = load_reference()

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(hn):
     for n in names:
         assert hasattr(lib, n), n
         assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
-    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 8
+    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 9
 
 
 def test_struct_sizes_match_header(hn):
@@ -48,7 +48,7 @@ def test_struct_layouts_match_compiled_header(hn, tmp_path):
     structs = {"hn_grid": L.HnGrid, "hn_mlp": L.HnMlp, "hn_mlp_grad": L.HnMlpGrad,
                "hn_render_cfg": L.HnRenderCfg, "hn_render_fwd_args": L.HnRenderFwdArgs,
                "hn_render_bwd_args": L.HnRenderBwdArgs, "hn_tv_args": L.HnTvArgs,
-               "hn_ray_sampler": L.HnRaySampler,
+               "hn_ray_sampler": L.HnRaySampler, "hn_ray_pool": L.HnRayPool,
                "hn_radam_tensor": L.HnRadamTensor}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hashnerf_amd.h"', "int main(void) {"]
     for cname, cls in structs.items():
@@ -85,6 +85,19 @@ def test_argument_validation_without_gpu(hn):
     a.n_rays = 4
     assert lib.hn_render_fwd(cfg, a, None, 0, None) == 2   # L != 16
     assert lib.hn_status_string(3).decode() == "workspace too small"
+    # ray pool: empty batch is a no-op, positions past the pool and bad shapes are rejected
+    p = L.HnRayPool()
+    p.n_images, p.H, p.W, p.pose_stride = 2, 4, 4, 16
+    assert lib.hn_sample_pool(p, None, None, None, 0, 0, None, None, None) == 0
+    assert lib.hn_sample_pool(p, None, None, None, 0, 8, None, None, None) == 1
+    x = C.c_void_p(16)   # never dereferenced: validation happens before any launch
+    assert lib.hn_sample_pool(p, x, x, x, 30, 8, x, x, None) == 2    # 30 + 8 > 2 * 4 * 4
+    p.pose_stride = 9
+    assert lib.hn_sample_pool(p, x, x, x, 0, 8, x, x, None) == 2
+    # blender images: odd size with half_res, bad mode
+    assert lib.hn_blender_images(x, 1, 5, 4, 1, 1, x, None) == 2
+    assert lib.hn_blender_images(x, 1, 4, 4, 0, 3, x, None) == 2
+    assert lib.hn_blender_images(None, 0, 4, 4, 1, 1, None, None) == 0
 
 
 def test_product_path_refuses_cpu_tensors(hn):
