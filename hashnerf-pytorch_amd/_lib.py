@@ -72,7 +72,7 @@ class HnRenderBwdArgs(C.Structure):
                 ("d_table_mode", C.c_int32), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
-                ("table_step", C.POINTER(HnRadamTensor))]
+                ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P)]
 
 
 class HnTvArgs(C.Structure):

@@ -4,28 +4,9 @@
 //     ops per level, including a sort-based embedding backward);
 //   * RAdam (radam.py:28-94): every parameter tensor in one launch, dense,
 //     in the reference's per-element op order.
-#include "hn_common.h"
+#include "hn_tv.h"
 
 namespace hn {
-
-struct TvK {
-  int32_t L, log2T;
-  int32_t cube[HN_MAX_LEVELS];
-  // packed 1-D grids: level l owns blocks [boff[l], boff[l+1]) of the
-  // forward (kTvFwdV vertices per thread) and [bofb[l], bofb[l+1]) of the
-  // backward (one thread per (vertex, feature)), instead of a (max blocks) x L
-  // grid that is mostly idle blocks
-  int32_t boff[HN_MAX_LEVELS + 1], bofb[HN_MAX_LEVELS + 1];
-  const int32_t* mv;
-  const float* table;
-};
-
-// Entry of grid vertex (x, y, z) of level l (hash_encoding.py:112-128).
-HN_DEV float2 tv_row(const TvK& k, int l, uint32_t x, uint32_t y, uint32_t z) {
-  const uint32_t mask = (1u << k.log2T) - 1u;
-  const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
-  return ld_row(k.table, (((uint32_t)l << k.log2T) + h) * 8u);
-}
 
 HN_DEV float block_sum_256(float v) {
   __shared__ float red[4];
@@ -34,20 +15,6 @@ HN_DEV float block_sum_256(float v) {
   __syncthreads();
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
-
-// level of packed block b (wave-uniform; at most 16 scalar compares)
-HN_DEV int tv_level(const TvK& k, const int32_t* off, int b) {
-  int l = 0;
-  while (l + 1 < k.L && b >= off[l + 1]) ++l;
-  return l;
-}
-
-// vertices per forward thread: fewer blocks, so fewer same-address atomics
-// on the 16 level sums
-#ifndef HN_TV_FWD_V
-#define HN_TV_FWD_V 4
-#endif
-constexpr int kTvFwdV = HN_TV_FWD_V;
 
 __global__ __launch_bounds__(256) void tv_fwd_kernel(TvK k, float* __restrict__ tv) {
   const int l = tv_level(k, k.boff, blockIdx.x);
@@ -77,12 +44,6 @@ __global__ __launch_bounds__(256) void tv_fwd_kernel(TvK k, float* __restrict__ 
 // One thread per (vertex, feature), x fastest: the two features of a row
 // are adjacent lanes and 8 consecutive x of one (y, z) share a 64-B segment,
 // so one wave-instruction of atomics is ~8 memory requests instead of 64.
-HN_DEV float tv_val(const TvK& k, int l, uint32_t x, uint32_t y, uint32_t z, int f) {
-  const uint32_t mask = (1u << k.log2T) - 1u;
-  const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
-  return k.table[((((size_t)l << k.log2T) + h) << 1) + f];
-}
-
 __global__ __launch_bounds__(256) void tv_bwd_kernel(TvK k, const float* __restrict__ g_tv,
                                                      float* __restrict__ dtable) {
   const int l = tv_level(k, k.bofb, blockIdx.x);
@@ -93,14 +54,7 @@ __global__ __launch_bounds__(256) void tv_bwd_kernel(TvK k, const float* __restr
   const int i = v % n1, j = (v / n1) % n1, kk = v / (n1 * n1);
   const uint32_t x = (uint32_t)(k.mv[3 * l] + i), y = (uint32_t)(k.mv[3 * l + 1] + j),
                  z = (uint32_t)(k.mv[3 * l + 2] + kk);
-  const float e = tv_val(k, l, x, y, z, f);
-  float g = 0.f;   // sum over incident edges of d(d^2)/de = -+2d
-  const int idx[3] = {i, j, kk};
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    if (idx[a] < c) g -= 2.f * (tv_val(k, l, x + (a == 0), y + (a == 1), z + (a == 2), f) - e);
-    if (idx[a] > 0) g += 2.f * (e - tv_val(k, l, x - (a == 0), y - (a == 1), z - (a == 2), f));
-  }
+  const float g = tv_grad(k, l, c, i, j, kk, x, y, z, f);
   const float scale = g_tv[l] / (float)c;
   const uint32_t mask = (1u << k.log2T) - 1u;
   const uint32_t h = (x ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask;
@@ -142,31 +96,6 @@ __global__ __launch_bounds__(256) void radam_kernel(RadamK k) {
       if (d.mode != 0) d.p[i] = p;
     }
   }
-}
-
-static int32_t make_tv(const hn_tv_args* a, TvK& k, int& fwd_blocks, int& bwd_blocks) {
-  if (!a || !a->min_vertex || !a->table) return HN_E_NULL;
-  if (a->n_levels < 1 || a->n_levels > HN_MAX_LEVELS) return HN_E_SHAPE;
-  if (a->log2_hashmap_size < 1 || a->log2_hashmap_size > 24) return HN_E_SHAPE;
-  k.L = a->n_levels;
-  k.log2T = a->log2_hashmap_size;
-  k.mv = a->min_vertex;
-  k.table = a->table;
-  for (int l = 0; l < HN_MAX_LEVELS; ++l) k.cube[l] = l < a->n_levels ? a->cube[l] : 1;
-  k.boff[0] = k.bofb[0] = 0;
-  for (int l = 0; l < HN_MAX_LEVELS; ++l) {
-    int nv = 0;
-    if (l < a->n_levels) {
-      const int c = a->cube[l];
-      if (c < 1 || c > 1000) return HN_E_SHAPE;
-      nv = (c + 1) * (c + 1) * (c + 1);
-    }
-    k.boff[l + 1] = k.boff[l] + (nv + 256 * kTvFwdV - 1) / (256 * kTvFwdV);
-    k.bofb[l + 1] = k.bofb[l] + (2 * nv + 255) / 256;
-  }
-  fwd_blocks = k.boff[a->n_levels];
-  bwd_blocks = k.bofb[a->n_levels];
-  return HN_OK;
 }
 
 }  // namespace hn

@@ -16,6 +16,7 @@
 // backward + float atomics into the hash-table gradient.
 #include "hn_mlp.h"
 #include "hn_render.h"
+#include "hn_tv.h"
 
 #include <math.h>
 #include <stdio.h>
@@ -741,10 +742,43 @@ HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
   }
 }
 
+// color_net.0 applied to the ray's sh features (the same for every point of
+// the ray): HN_C0SH_LDS 1 keeps its 64 rows in the wave's LDS slab after the
+// images (read back as the c0 accumulators' seed, 8 broadcast ds_read_b128
+// per tile) instead of 32 VGPRs live across the unit's tiles.
+#ifndef HN_C0SH_LDS
+#define HN_C0SH_LDS 1
+#endif
+constexpr int kC0shF = kNImg * kImgBlk / 4;   // float offset in the wave's slab
+static_assert(kC0shF + 64 <= kRRows * kXS, "c0sh fits the per-wave slab");
+struct C0Sh {
+#if HN_C0SH_LDS
+  const float* lds;
+#else
+  f32x16 v[2];
+#endif
+};
+HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
+#if HN_C0SH_LDS
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(c.lds + 32 * ob + row_of(4 * g, h));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c0[ob][4 * g + j] = v[j];
+    }
+#else
+  (void)h;
+  c0[0] = c.v[0];
+  c0[1] = c.v[1];
+#endif
+}
+
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
-                      const f32x16 c0sh[2], float4 dr, DW& dw) {
+                      const C0Sh& c0sh, float4 dr, DW& dw) {
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
   const int h = lane >> 5;
   char* Xb = reinterpret_cast<char*>(X);
@@ -756,7 +790,8 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   relu_bits(h0[0], mh0, 0);
   relu_bits(h0[1], mh0, 1);
   const f32x16 s1 = gemm_w<seg_of(R_F1), kBH0>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; }, Xb);
-  f32x16 c0[2] = {c0sh[0], c0sh[1]};
+  f32x16 c0[2];
+  c0sh_seed(c0sh, c0, h);
   // s1 rows 0..15 = [sigma | geo15] -> features 16..31 of [sh16 | sigma | geo15]
   gemm2<R_F2G, kBC0in, 4>(wr, P, c0, lane, [&](int s) { return s1[s]; }, Xb);
   relu_bits(c0[0], mc0, 0);
@@ -1343,18 +1378,25 @@ __host__ __device__ inline int64_t sc_units_per_block(int64_t n_rays) {   // sca
   return (3 * (n_rays > 0 ? n_rays : 1) + kBwdBlocks - 1) / kBwdBlocks;
 }
 __host__ __device__ inline size_t ovf_per_block(int64_t n_rays) { return (size_t)sc_units_per_block(n_rays) * 64 * 64; }
+// TV records (the table's total-variation term, loss.py:11-43, folded into the
+// owner pass): one record per x-pair of cube vertices, at most 16 levels x
+// ceil(51 / 2) x 51 x 51 (cube edges <= 50, loss.py:20-22).  They form one
+// more overflow list (producer kBwdBlocks) right after the blocks' lists, so
+// ovf_place_kernel buckets them by bin like spilled records.
+constexpr int kTvMaxCube = 50;
+constexpr size_t kTvRecCap = (size_t)16 * ((kTvMaxCube + 2) / 2) * (kTvMaxCube + 1) * (kTvMaxCube + 1);
 __host__ __device__ inline size_t bin_records(int nbins, int cap, int64_t n_rays) {
-  return (size_t)kBwdBlocks * nbins * cap + (size_t)kBwdBlocks * ovf_per_block(n_rays);
+  return (size_t)kBwdBlocks * nbins * cap + (size_t)kBwdBlocks * ovf_per_block(n_rays) + kTvRecCap;
 }
 // Overflow book, u32 words after the counts and level maxima (idx + nrec +
 // kBwdBlocks * (nbins + 16)): total spilled, spilled per bin, placement
 // cursors, first slot per bin, spilled per producer block, record ids
 // (relative to the first overflow record) bucketed by bin.
 struct OvfBook {
-  uint32_t *cnt, *per_bin, *cur, *first, *blk, *ids;
+  uint32_t *cnt, *per_bin, *cur, *first, *blk, *tvmx, *ids;
 };
 __host__ __device__ inline size_t ovf_book_words(int nbins, int64_t n_rays) {
-  return 1 + 3 * (size_t)nbins + kBwdBlocks + (size_t)kBwdBlocks * ovf_per_block(n_rays);
+  return 1 + 3 * (size_t)nbins + (kBwdBlocks + 1) + 16 + (size_t)kBwdBlocks * ovf_per_block(n_rays) + kTvRecCap;
 }
 __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbins) {
   OvfBook o;
@@ -1362,8 +1404,9 @@ __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbin
   o.per_bin = o.cnt + 1;
   o.cur = o.per_bin + nbins;
   o.first = o.cur + nbins;
-  o.blk = o.first + nbins;
-  o.ids = o.blk + kBwdBlocks;
+  o.blk = o.first + nbins;          // [kBwdBlocks + 1]: the last one counts the TV records
+  o.tvmx = o.blk + kBwdBlocks + 1;   // [16] largest |TV record value| per level (float bits)
+  o.ids = o.tvmx + 16;
   return o;
 }
 
@@ -1669,6 +1712,71 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
 }
 
+// ---- TV term as records (loss.py:11-43 backward into the owner pass) ------
+// The table's total-variation gradient (tv_grad: per cube vertex, scaled by
+// g_tv[l] / cube) goes into the bins like the render scatter's: one record per
+// x-pair of cube vertices (x0, x0 + 1) of one (y, z) row, in the same 20-B
+// format, written to the TV list (the last overflow list: producer
+// kBwdBlocks) at a fixed index, counted per bin for ovf_place_kernel, and its
+// per-level largest |value| kept for the owner's fixed-point scale.  So the
+// TV step keeps the table's RAdam step fused and the gradient unstored.
+// Thread layout: the levels' pairs at 64-aligned offsets (one level per wave).
+struct TvRecK {
+  TvK tv;
+  int32_t pad_off[17];    // first thread of level l (64-aligned)
+  int32_t rec_off[17];    // first record of level l in the TV list (dense)
+  const float* g_tv;
+  float* bins;
+  int32_t nbins, bin_cap, bin_shift;
+  int64_t B;
+};
+__global__ __launch_bounds__(256) void tv_rec_kernel(TvRecK k) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int L = k.tv.L;
+  if (t >= k.pad_off[L]) return;                      // whole waves: pad_off is 64-aligned
+  int l = 0;
+  while (l + 1 < L && t >= k.pad_off[l + 1]) ++l;     // wave-uniform
+  const int c = k.tv.cube[l], n1 = c + 1, np = (n1 + 1) / 2;
+  const int loc = t - k.pad_off[l];
+  const bool on = loc < np * n1 * n1;
+  const int ip = loc % np, j = (loc / np) % n1, kk = loc / (np * n1);
+  const uint32_t x0 = (uint32_t)(k.tv.mv[3 * l] + 2 * ip), y = (uint32_t)(k.tv.mv[3 * l + 1] + j),
+                 z = (uint32_t)(k.tv.mv[3 * l + 2] + kk);
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (on) {
+    const float scale = k.g_tv[l] / (float)c;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) v[f] = scale * tv_grad(k.tv, l, c, 2 * ip, j, kk, x0, y, z, f);
+    if (2 * ip + 1 <= c)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) v[2 + f] = scale * tv_grad(k.tv, l, c, 2 * ip + 1, j, kk, x0 + 1u, y, z, f);
+  }
+  const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
+  uint32_t* const book = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
+  const OvfBook ob = ovf_book(book, nrec, k.nbins);
+  const float vmax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+  const float chk = (v[0] + v[1]) + (v[2] + v[3]);
+  if (__ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && (threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float wmax = wave_max_f32(vmax);
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_max(ob.tvmx + l, __float_as_uint(wmax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!on) return;
+  const uint32_t mask = (1u << k.tv.log2T) - 1u;
+  const uint32_t flat = ((uint32_t)l << k.tv.log2T) + ((x0 ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask);
+  const uint32_t nbits = (uint32_t)__builtin_ctz(~x0) + 1u;
+  const size_t r = (size_t)kBwdBlocks * k.nbins * k.bin_cap + (size_t)kBwdBlocks * ovf_per_block(k.B) +
+                   (size_t)(k.rec_off[l] + loc);
+  *reinterpret_cast<f32x4*>(k.bins + rec_vofs(r)) = f32x4{v[0], v[1], v[2], v[3]};
+  reinterpret_cast<uint32_t*>(k.bins)[rec_wofs(r, nrec)] = flat | (nbits << 28);
+  __hip_atomic_fetch_add(ob.per_bin + (flat >> k.bin_shift), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {
+    const uint32_t n = (uint32_t)k.rec_off[L];
+    ob.blk[kBwdBlocks] = n;
+    __hip_atomic_fetch_add(ob.cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // The table-gradient scatter of one slot (embedding_dense_backward of
 // hash_encoding.py:106 + trilinear backward); V = 2048-float voxel buffer.
 template <int CAP>
@@ -1897,10 +2005,27 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
   // color_net.0 applied to the sh part: the same for every point of the ray
   // (and bit-identical to starting each point's chain with it)
-  f32x16 c0sh[2];
+  C0Sh c0sh;
+#if HN_C0SH_LDS
+  {
+    float* cl = X + kC0shF;
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) {
+      const f32x16 v = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+      if (p == 0)   // every point's column holds the same rows: lanes 0 and 32 store them
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(cl + 32 * ob + row_of(4 * g, h)) =
+              f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+    }
+    lds_fence_wave();
+    c0sh.lds = cl;
+  }
+#else
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob)
-    c0sh[ob] = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+    c0sh.v[ob] = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+#endif
   const int ctile = (fine ? kSc / 32 : 0) + tile0;
   float zq[2] = {0.f, 0.f};
   int srcq[2] = {0, 0};
@@ -1979,8 +2104,9 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0) {   // binned scatter: no overflow records yet (count, per bin, cursors)
     const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
-    uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
-    for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
+    const OvfBook ob = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins);
+    for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) ob.cnt[i] = 0u;
+    if (threadIdx.x < 17) ob.blk[kBwdBlocks + threadIdx.x] = 0u;   // TV count, TV level maxima
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -2468,6 +2594,8 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     const uint32_t c = cnt[(size_t)b * kBwdBlocks + threadIdx.x];
     n = c < (uint32_t)k.cap ? c : (uint32_t)k.cap;
     for (int l = lev0; l < lev0 + nlev; ++l) mx = fmaxf(mx, mxs[l * kBwdBlocks + threadIdx.x]);
+    if (threadIdx.x == 0)   // the TV records' level maxima (tv_rec_kernel; 0 without a TV term)
+      for (int l = lev0; l < lev0 + nlev; ++l) mx = fmaxf(mx, __uint_as_float(obk.tvmx[l]));
   }
   const uint32_t inc = (uint32_t)wave_incl_sum((double)n);   // exact: counts < 2^53
   const float wmx = wave_max_f32(mx);
@@ -2843,6 +2971,23 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     if (mode != kModeSplit || ts.n != ((int64_t)16 << cfg->grid.log2_hashmap_size) * 2) return HN_E_SHAPE;
     if (!ts.p || !ts.m || !ts.v) return HN_E_NULL;
   }
+  // TV term: records into the bins (binned, cubes <= kTvMaxCube) or hn_tv_bwd into d_table
+  TvRecK tk;
+  bool tv_rec = false, tv_atomic = false;
+  if (a->tv) {
+    if (!a->g_tv) return HN_E_NULL;
+    int nbf, nbb;
+    if ((st = make_tv(a->tv, tk.tv, nbf, nbb))) return st;
+    if (a->tv->n_levels != cfg->grid.n_levels || a->tv->log2_hashmap_size != T) return HN_E_SHAPE;
+    bool small = true;
+    for (int l = 0; l < a->tv->n_levels; ++l) small = small && a->tv->cube[l] <= kTvMaxCube;
+    if (mode == kModeSplit && small) {
+      tv_rec = true;
+    } else {
+      if (a->table_step || !a->d_table) return HN_E_SHAPE;
+      tv_atomic = true;
+    }
+  }
   const WsLayout wl = ws_layout(cfg, a->n_rays, mode);
   BinGeom bg{};
   k.bins = nullptr;
@@ -2860,6 +3005,26 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   }
   hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
                      dim3(64 * kFwdWaves), 0, s, k);
+  if (tv_rec) {   // after the pre-pass has cleared the overflow book
+    int po = 0, ro = 0;
+    const int L = a->tv->n_levels;
+    for (int l = 0; l < L; ++l) {
+      tk.pad_off[l] = po;
+      tk.rec_off[l] = ro;
+      const int n1 = a->tv->cube[l] + 1, cnt = (n1 + 1) / 2 * n1 * n1;
+      ro += cnt;
+      po += (cnt + 63) & ~63;
+    }
+    tk.pad_off[L] = po;
+    tk.rec_off[L] = ro;
+    tk.g_tv = a->g_tv;
+    tk.bins = k.bins;
+    tk.nbins = k.nbins;
+    tk.bin_cap = k.bin_cap;
+    tk.bin_shift = k.bin_shift;
+    tk.B = a->n_rays;
+    hipLaunchKernelGGL(tv_rec_kernel, dim3((unsigned)((po + 255) / 256)), dim3(256), 0, s, tk);
+  }
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
   if (mode == kModeSplit)
@@ -2901,7 +3066,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.overwrite = (a->d_table_mode & 1) != 0;
     r.fused = a->table_step != nullptr;
     if (r.fused) r.step = *a->table_step;
-    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
+    // one block per producer's overflow list, + the TV list
+    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks + 1), dim3(kPlaceThreads), 0, s, r);
     if ((st = hip_status(hipGetLastError()))) return st;
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
                        (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
@@ -2941,5 +3107,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
 #endif
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,
                      a->d_coarse, a->d_fine, (a->d_table_mode & 2) ? 1 : 0);
-  return hip_status(hipGetLastError());
+  if ((st = hip_status(hipGetLastError()))) return st;
+  if (tv_atomic) return hn_tv_bwd(a->tv, a->g_tv, a->d_table, stream);
+  return HN_OK;
 }

@@ -259,7 +259,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
 
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
-               overwrite_mlp: bool = False):
+               overwrite_mlp: bool = False, tv=None):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -267,7 +267,11 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     of g_rgb, g_depth, g_acc, g_sparsity, g_rgb0, g_depth0, g_acc0,
     g_sparsity0, g_raw_f (missing = 0).  table_step = (table, exp_avg,
     exp_avg_sq, coeffs) from RAdam.take_step: the binned owner pass applies
-    that RAdam step to the table with this gradient (d_table may be None)."""
+    that RAdam step to the table with this gradient (d_table may be None).
+    tv = (min_vertex [L, 3] device int32, cubes, g_tv [L]) from tv_fwd and the
+    loss backward: the TV term's table gradient (loss.py:11-43) joins this
+    backward -- as records of the binned owner pass (so table_step stays
+    fused), or added to d_table -- instead of a separate tv_bwd."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -303,6 +307,14 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
                   "mode", "has_wd"):
             setattr(step, k, c[k])
         a.table_step = C.pointer(step)
+    if tv is not None:
+        mv, cubes, g_tv = tv
+        tva = _tv_args(st.table, mv, cubes, st.cfg.grid.log2_hashmap_size)
+        keep.append(tva)
+        a.tv = C.cast(C.pointer(tva), C.c_void_p)
+        g_tv = g_tv.contiguous()
+        keep.append(g_tv)
+        a.g_tv = g_tv.data_ptr()
     t0 = TIMER.begin("render_bwd")
     L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
     TIMER.end("render_bwd", t0)

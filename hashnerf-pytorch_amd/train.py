@@ -421,20 +421,21 @@ class Trainer:
         # the ten MLP grads (one flat buffer) are written, not accumulated:
         # no zero fill
         grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)
-        if self.fuse_table_step and self.world == 1 and tv is None and self._binned:
-            # one GPU, no TV term: the table gradient is complete where the
+        # the TV term's table gradient joins the render backward (records of
+        # the binned owner pass, or added to the stored gradient)
+        tvb = None if tv is None else (mv, cubes, g_tv)
+        if self.fuse_table_step and self.world == 1 and self._binned:
+            # one GPU: the table gradient (render + TV) is complete where the
             # binned owner pass forms it, so the table's RAdam step runs there
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True)
+                          overwrite_mlp=True, tv=tvb)
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
-            # no zero fill of the 64 MiB buffer); TV then accumulates into it
-            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True)
-            if tv is not None:
-                HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
+            # no zero fill of the 64 MiB buffer), TV included
+            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True, tv=tvb)
             table.grad = self._gtable
         for p, g in zip(self._ws, self._gws):
             p.grad = g

@@ -204,6 +204,14 @@ typedef struct hn_render_bwd_args {
    * the gradient; p / m / v are the table and its moments, g is ignored.
    * NULL = no step (the gradient goes to d_table). */
   const struct hn_radam_tensor* table_step;
+  /* Optional total-variation term (loss.py:11-43; run_nerf.py:626-635) in the same
+   * backward (ABI 9): tv = the TV args of the hn_tv_fwd call (host), g_tv = device
+   * [L] upstream gradients of its per-level values.  With the binned scatter and
+   * cubes <= 50 its gradient goes into the bins as records (so table_step stays
+   * fused); otherwise it is added to d_table (hn_tv_bwd; table_step not allowed).
+   * NULL = no TV term. */
+  const struct hn_tv_args* tv;
+  const float* g_tv;
 } hn_render_bwd_args;
 
 /* ---- L4 hash-table total variation (loss.py:11-43), all levels at once ---

@@ -152,6 +152,7 @@ def test_trainer_explicit_matches_autograd(hn):
         args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=10,
                             sparse_loss_weight=1e-3)
         tr = Trainer(args, data, DEV, mode=mode)
+        tr.fuse_table_step = False           # keep the table gradient to compare
         torch.manual_seed(123)
         loss, mse = tr.step()
         res[mode] = (float(loss.detach()), float(mse), tr.embed_fn.table.grad.clone(),
@@ -183,18 +184,21 @@ def test_trainer_step_index_follows_reference_loop(hn):
     assert default_args().tv_until == 1001            # run_nerf.py:636-638: TV through i = 1001
 
 
-def test_trainer_fused_table_step_bitwise(hn):
+@pytest.mark.parametrize("tv", [0.0, 1e-4])
+def test_trainer_fused_table_step_bitwise(hn, tv):
     """the trainer path that fuses the table's RAdam step into the
     binned owner pass (take_step -> render_bwd(table_step) -> step() of the
     MLP groups only) against the unfused path (gradient stored, hn_radam_step)
     from the same seed: table, moments and step counters bitwise equal after
-    8 steps (the update starts at step 6, N_sma >= 5).  No TV term, so the
-    fused branch is the one taken."""
+    8 steps (the update starts at step 6, N_sma >= 5), without and with a TV
+    term (whose gradient joins the owner pass as records, so the fused branch
+    is taken in both)."""
     from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
     data = SyntheticBlender(64, 64, 4, DEV, seed=0)
     res = {}
     for fuse in (True, False):
-        args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=0.0, sparse_loss_weight=1e-3)
+        args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=tv, tv_until=10 ** 6,
+                            sparse_loss_weight=1e-3)
         tr = Trainer(args, data, DEV, seed=3)
         tr.fuse_table_step = fuse
         torch.manual_seed(11)
