@@ -777,8 +777,12 @@ HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
 
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
+// after_fwd(): called once the forward recompute is done (its activations
+// live on only as LDS images and mask bits) -- where the next unit's prefetch
+// adds the fewest live registers.
+template <typename AfterFwd>
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
-                      const C0Sh& c0sh, float4 dr, DW& dw) {
+                      const C0Sh& c0sh, float4 dr, DW& dw, AfterFwd&& after_fwd) {
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
   const int h = lane >> 5;
   char* Xb = reinterpret_cast<char*>(X);
@@ -812,6 +816,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
       put_quad(Xb, kBDR, q, lane & 31, 0, w[0], w[1]);
     }
   }
+  after_fwd();
   lds_fence_wave();
   // ---- color_net.2 (dW rows >= 3 are discarded) ----
   {
@@ -1378,25 +1383,18 @@ __host__ __device__ inline int64_t sc_units_per_block(int64_t n_rays) {   // sca
   return (3 * (n_rays > 0 ? n_rays : 1) + kBwdBlocks - 1) / kBwdBlocks;
 }
 __host__ __device__ inline size_t ovf_per_block(int64_t n_rays) { return (size_t)sc_units_per_block(n_rays) * 64 * 64; }
-// TV records (the table's total-variation term, loss.py:11-43, folded into the
-// owner pass): one record per x-pair of cube vertices, at most 16 levels x
-// ceil(51 / 2) x 51 x 51 (cube edges <= 50, loss.py:20-22).  They form one
-// more overflow list (producer kBwdBlocks) right after the blocks' lists, so
-// ovf_place_kernel buckets them by bin like spilled records.
-constexpr int kTvMaxCube = 50;
-constexpr size_t kTvRecCap = (size_t)16 * ((kTvMaxCube + 2) / 2) * (kTvMaxCube + 1) * (kTvMaxCube + 1);
 __host__ __device__ inline size_t bin_records(int nbins, int cap, int64_t n_rays) {
-  return (size_t)kBwdBlocks * nbins * cap + (size_t)kBwdBlocks * ovf_per_block(n_rays) + kTvRecCap;
+  return (size_t)kBwdBlocks * nbins * cap + (size_t)kBwdBlocks * ovf_per_block(n_rays);
 }
 // Overflow book, u32 words after the counts and level maxima (idx + nrec +
 // kBwdBlocks * (nbins + 16)): total spilled, spilled per bin, placement
 // cursors, first slot per bin, spilled per producer block, record ids
 // (relative to the first overflow record) bucketed by bin.
 struct OvfBook {
-  uint32_t *cnt, *per_bin, *cur, *first, *blk, *tvmx, *ids;
+  uint32_t *cnt, *per_bin, *cur, *first, *blk, *ids;
 };
 __host__ __device__ inline size_t ovf_book_words(int nbins, int64_t n_rays) {
-  return 1 + 3 * (size_t)nbins + (kBwdBlocks + 1) + 16 + (size_t)kBwdBlocks * ovf_per_block(n_rays) + kTvRecCap;
+  return 1 + 3 * (size_t)nbins + kBwdBlocks + (size_t)kBwdBlocks * ovf_per_block(n_rays);
 }
 __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbins) {
   OvfBook o;
@@ -1404,9 +1402,8 @@ __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbin
   o.per_bin = o.cnt + 1;
   o.cur = o.per_bin + nbins;
   o.first = o.cur + nbins;
-  o.blk = o.first + nbins;          // [kBwdBlocks + 1]: the last one counts the TV records
-  o.tvmx = o.blk + kBwdBlocks + 1;   // [16] largest |TV record value| per level (float bits)
-  o.ids = o.tvmx + 16;
+  o.blk = o.first + nbins;
+  o.ids = o.blk + kBwdBlocks;
   return o;
 }
 
@@ -1528,6 +1525,12 @@ struct ScK {
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   int32_t scramble;       // render_bwd_kernel's Feistel half-width (HN_SC_PERM), 0: identity
+  // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
+  // x-pair of level l (tv_off[L] pairs in all; 0 = no TV term), split evenly
+  // over the blocks after their units
+  int32_t tv_off[17];
+  const float* g_tv;
+  TvK tv;
 };
 #ifndef HN_SC_PERM       // 1: a block's rays through the backward's batch permutation
 #define HN_SC_PERM 0
@@ -1686,6 +1689,38 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 #endif
     }
   }
+  if (k.tv_off[16] > 0) {
+    // The TV term's table gradient: one record per x-pair (x0, x0 + 1) of cube
+    // vertices of one (y, z) row, d TV_l / d e (tv_grad) scaled by g_tv[l] /
+    // cube, through the same region / overflow path as the render records
+    // (so the owner pass sums render + TV exactly and the table step stays fused)
+    const int total = k.tv_off[16], per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int q0 = (int)blockIdx.x * per, q1 = q0 + per < total ? q0 + per : total;
+    const uint32_t T = (uint32_t)k.g.log2T;
+    for (int q = q0 + (int)threadIdx.x; q < q1; q += (int)blockDim.x) {
+      int l = 0;
+      while (l + 1 < k.tv.L && q >= k.tv_off[l + 1]) ++l;
+      const int c = k.tv.cube[l], n1 = c + 1, np = (n1 + 1) / 2, loc = q - k.tv_off[l];
+      const int ip = loc % np, j = (loc / np) % n1, kk = loc / (np * n1);
+      const uint32_t x0 = (uint32_t)(k.tv.mv[3 * l] + 2 * ip), y = (uint32_t)(k.tv.mv[3 * l + 1] + j),
+                     z = (uint32_t)(k.tv.mv[3 * l + 2] + kk);
+      const float scale = k.g_tv[l] / (float)c;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f = 0; f < 2; ++f) v[f] = scale * tv_grad(k.tv, l, c, 2 * ip, j, kk, x0, y, z, f);
+      if (2 * ip + 1 <= c)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) v[2 + f] = scale * tv_grad(k.tv, l, c, 2 * ip + 1, j, kk, x0 + 1u, y, z, f);
+      const float chk = (v[0] + v[1]) + (v[2] + v[3]);
+      if (!(fabsf(chk) <= 3.402823466e38f))
+        __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float vmax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+      __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      const RecSlot rs = rec_slot(bw, (uint32_t)l, T, x0, y * kPrimeY, z * kPrimeZ);
+      rec_store(bw, rs, v);
+    }
+  }
   __syncthreads();
 #if HN_SC_LANEMAX
   if (wave == 0) {   // lane = level: the max of its 64 lane slots
@@ -1709,71 +1744,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     const uint32_t n = lovf < bw.n_ovf ? lovf : bw.n_ovf;
     ob.blk[blockIdx.x] = n;
     if (n) __hip_atomic_fetch_add(ob.cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ---- TV term as records (loss.py:11-43 backward into the owner pass) ------
-// The table's total-variation gradient (tv_grad: per cube vertex, scaled by
-// g_tv[l] / cube) goes into the bins like the render scatter's: one record per
-// x-pair of cube vertices (x0, x0 + 1) of one (y, z) row, in the same 20-B
-// format, written to the TV list (the last overflow list: producer
-// kBwdBlocks) at a fixed index, counted per bin for ovf_place_kernel, and its
-// per-level largest |value| kept for the owner's fixed-point scale.  So the
-// TV step keeps the table's RAdam step fused and the gradient unstored.
-// Thread layout: the levels' pairs at 64-aligned offsets (one level per wave).
-struct TvRecK {
-  TvK tv;
-  int32_t pad_off[17];    // first thread of level l (64-aligned)
-  int32_t rec_off[17];    // first record of level l in the TV list (dense)
-  const float* g_tv;
-  float* bins;
-  int32_t nbins, bin_cap, bin_shift;
-  int64_t B;
-};
-__global__ __launch_bounds__(256) void tv_rec_kernel(TvRecK k) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  const int L = k.tv.L;
-  if (t >= k.pad_off[L]) return;                      // whole waves: pad_off is 64-aligned
-  int l = 0;
-  while (l + 1 < L && t >= k.pad_off[l + 1]) ++l;     // wave-uniform
-  const int c = k.tv.cube[l], n1 = c + 1, np = (n1 + 1) / 2;
-  const int loc = t - k.pad_off[l];
-  const bool on = loc < np * n1 * n1;
-  const int ip = loc % np, j = (loc / np) % n1, kk = loc / (np * n1);
-  const uint32_t x0 = (uint32_t)(k.tv.mv[3 * l] + 2 * ip), y = (uint32_t)(k.tv.mv[3 * l + 1] + j),
-                 z = (uint32_t)(k.tv.mv[3 * l + 2] + kk);
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  if (on) {
-    const float scale = k.g_tv[l] / (float)c;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) v[f] = scale * tv_grad(k.tv, l, c, 2 * ip, j, kk, x0, y, z, f);
-    if (2 * ip + 1 <= c)
-#pragma unroll
-      for (int f = 0; f < 2; ++f) v[2 + f] = scale * tv_grad(k.tv, l, c, 2 * ip + 1, j, kk, x0 + 1u, y, z, f);
-  }
-  const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
-  uint32_t* const book = reinterpret_cast<uint32_t*>(k.bins + 4 * nrec);
-  const OvfBook ob = ovf_book(book, nrec, k.nbins);
-  const float vmax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-  const float chk = (v[0] + v[1]) + (v[2] + v[3]);
-  if (__ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && (threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const float wmax = wave_max_f32(vmax);
-  if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_max(ob.tvmx + l, __float_as_uint(wmax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!on) return;
-  const uint32_t mask = (1u << k.tv.log2T) - 1u;
-  const uint32_t flat = ((uint32_t)l << k.tv.log2T) + ((x0 ^ (y * kPrimeY) ^ (z * kPrimeZ)) & mask);
-  const uint32_t nbits = (uint32_t)__builtin_ctz(~x0) + 1u;
-  const size_t r = (size_t)kBwdBlocks * k.nbins * k.bin_cap + (size_t)kBwdBlocks * ovf_per_block(k.B) +
-                   (size_t)(k.rec_off[l] + loc);
-  *reinterpret_cast<f32x4*>(k.bins + rec_vofs(r)) = f32x4{v[0], v[1], v[2], v[3]};
-  reinterpret_cast<uint32_t*>(k.bins)[rec_wofs(r, nrec)] = flat | (nbits << 28);
-  __hip_atomic_fetch_add(ob.per_bin + (flat >> k.bin_shift), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t == 0) {
-    const uint32_t n = (uint32_t)k.rec_off[L];
-    ob.blk[kBwdBlocks] = n;
-    __hip_atomic_fetch_add(ob.cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1977,15 +1947,38 @@ HN_DEV void wait_flag(int* flag, int need) {
 // Fine units hand each tile to the scatter wave; before the first hand-off
 // they wait until wave 0 has published this ray's coarse feature grads
 // (*done >= need)
+// Split schedule: a wave's units are known in advance (static split), so the
+// next unit's first inputs -- its first tile's saved features and its ray's
+// view direction -- are loaded while the current unit's second tile runs,
+// instead of exposing their HBM latency at every unit start (HN_B1_PREFETCH).
+#ifndef HN_B1_PREFETCH
+#define HN_B1_PREFETCH 0
+#endif
+struct UnitPre {
+  f32x16 feat;      // this unit's first-tile features (loaded by the previous unit)
+  float vd[3];      // this unit's view direction
+  int64_t next;     // the next unit's ray, or -1
+};
+HN_DEV void unit_pre_load(const B1K& k, int64_t ray, int ctile, int lane, UnitPre& u) {
+  load_feat(k.feat, ray, ctile, lane, u.feat);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) u.vd[a] = k.rays[11 * ray + 8 + a];
+}
+
 template <int S, int MODE>
 HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const Ring* ring,
-                    PhaseClock& pc, int* done = nullptr, int need = 0) {
+                    PhaseClock& pc, int* done = nullptr, int need = 0, UnitPre* pre = nullptr) {
   pc.start();
   const int lane = lane_id();
   constexpr bool fine = S == kSf;
   const int p = lane & 31, h = lane >> 5;
   Ray r;
-  load_ray(k.rays, ray, r);
+  if (pre != nullptr) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) r.vd[a] = pre->vd[a];   // the split backward needs only the view direction
+  } else {
+    load_ray(k.rays, ray, r);
+  }
   const int tile0 = 2 * part;                   // tile within this pass
   const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
   float4 dr[2];
@@ -2037,7 +2030,10 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
     }
   }
   f32x16 feat, featn;
-  load_feat(k.feat, ray, ctile, lane, feat);
+  if (pre != nullptr)
+    feat = pre->feat;
+  else
+    load_feat(k.feat, ray, ctile, lane, feat);
   load_feat(k.feat, ray, ctile + 1, lane, featn);
   static_for<0, 2>([&](auto tc) {   // unrolled: the ring's slots and the per-tile arrays stay static
     constexpr int t = decltype(tc)::value;
@@ -2047,7 +2043,10 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 #pragma unroll
     for (int r = 0; r < 16; ++r) dfeat[r] *= dr[t].x;
 #else
-    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw);
+    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw, [&]() {
+      if (t == 1 && pre != nullptr && pre->next >= 0)   // the next unit's first inputs, during tile 1
+        unit_pre_load(k, pre->next, ctile, lane, *pre);
+    });
 #endif
     HN_LAP(pc, mlp);
     const int qbase = 32 * (tile0 + t);
@@ -2104,9 +2103,8 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0) {   // binned scatter: no overflow records yet (count, per bin, cursors)
     const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
-    const OvfBook ob = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins);
-    for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) ob.cnt[i] = 0u;
-    if (threadIdx.x < 17) ob.blk[kBwdBlocks + threadIdx.x] = 0u;   // TV count, TV level maxima
+    uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
+    for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -2273,10 +2271,14 @@ void render_bwd_kernel(B1K k) {
     if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
 #endif
   } else {
+    UnitPre pre;
+    UnitPre* prep = SPLIT && HN_B1_PREFETCH ? &pre : nullptr;
     if (wave == 0) {
       wring_prime(wr, k.Pc, lane);
+      if (prep && n_rays > 0) unit_pre_load(k, block_ray(0), 0, lane, pre);
       for (int i = 0; i < n_rays; ++i) {
-        b1_unit<kSc, MODE>(k, block_ray(i), 0, X, dw, wr, nullptr, pc);
+        pre.next = i + 1 < n_rays ? block_ray(i + 1) : -1;
+        b1_unit<kSc, MODE>(k, block_ray(i), 0, X, dw, wr, nullptr, pc, nullptr, 0, prep);
         if constexpr (!SPLIT) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this ray's feature grads are in L2
           if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2293,8 +2295,11 @@ void render_bwd_kernel(B1K k) {
       // dW slab, and with the fixed-order slab reduce the MLP gradients, are
       // bitwise reproducible
       wring_prime(wr, k.Pf, lane);
-      for (int i = 0; i < n_rays; ++i)
-        b1_unit<kSf, MODE>(k, block_ray(i), wave - 1, X, dw, wr, &ring, pc, &sync[0], i + 1);
+      if (prep && n_rays > 0) unit_pre_load(k, block_ray(0), kSc / 32 + 2 * (wave - 1), lane, pre);
+      for (int i = 0; i < n_rays; ++i) {
+        pre.next = i + 1 < n_rays ? block_ray(i + 1) : -1;
+        b1_unit<kSf, MODE>(k, block_ray(i), wave - 1, X, dw, wr, &ring, pc, &sync[0], i + 1, prep);
+      }
     } else if (!SPLIT) {
       wring_prime(wr, k.Pf, lane);
       for (;;) {
@@ -2594,8 +2599,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     const uint32_t c = cnt[(size_t)b * kBwdBlocks + threadIdx.x];
     n = c < (uint32_t)k.cap ? c : (uint32_t)k.cap;
     for (int l = lev0; l < lev0 + nlev; ++l) mx = fmaxf(mx, mxs[l * kBwdBlocks + threadIdx.x]);
-    if (threadIdx.x == 0)   // the TV records' level maxima (tv_rec_kernel; 0 without a TV term)
-      for (int l = lev0; l < lev0 + nlev; ++l) mx = fmaxf(mx, __uint_as_float(obk.tvmx[l]));
   }
   const uint32_t inc = (uint32_t)wave_incl_sum((double)n);   // exact: counts < 2^53
   const float wmx = wave_max_f32(mx);
@@ -2971,17 +2974,15 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     if (mode != kModeSplit || ts.n != ((int64_t)16 << cfg->grid.log2_hashmap_size) * 2) return HN_E_SHAPE;
     if (!ts.p || !ts.m || !ts.v) return HN_E_NULL;
   }
-  // TV term: records into the bins (binned, cubes <= kTvMaxCube) or hn_tv_bwd into d_table
-  TvRecK tk;
+  // TV term: records of the binned scatter, or hn_tv_bwd into d_table (atomic schedule)
+  TvK tvk;
   bool tv_rec = false, tv_atomic = false;
   if (a->tv) {
     if (!a->g_tv) return HN_E_NULL;
     int nbf, nbb;
-    if ((st = make_tv(a->tv, tk.tv, nbf, nbb))) return st;
+    if ((st = make_tv(a->tv, tvk, nbf, nbb))) return st;
     if (a->tv->n_levels != cfg->grid.n_levels || a->tv->log2_hashmap_size != T) return HN_E_SHAPE;
-    bool small = true;
-    for (int l = 0; l < a->tv->n_levels; ++l) small = small && a->tv->cube[l] <= kTvMaxCube;
-    if (mode == kModeSplit && small) {
+    if (mode == kModeSplit) {
       tv_rec = true;
     } else {
       if (a->table_step || !a->d_table) return HN_E_SHAPE;
@@ -3005,26 +3006,6 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   }
   hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
                      dim3(64 * kFwdWaves), 0, s, k);
-  if (tv_rec) {   // after the pre-pass has cleared the overflow book
-    int po = 0, ro = 0;
-    const int L = a->tv->n_levels;
-    for (int l = 0; l < L; ++l) {
-      tk.pad_off[l] = po;
-      tk.rec_off[l] = ro;
-      const int n1 = a->tv->cube[l] + 1, cnt = (n1 + 1) / 2 * n1 * n1;
-      ro += cnt;
-      po += (cnt + 63) & ~63;
-    }
-    tk.pad_off[L] = po;
-    tk.rec_off[L] = ro;
-    tk.g_tv = a->g_tv;
-    tk.bins = k.bins;
-    tk.nbins = k.nbins;
-    tk.bin_cap = k.bin_cap;
-    tk.bin_shift = k.bin_shift;
-    tk.B = a->n_rays;
-    hipLaunchKernelGGL(tv_rec_kernel, dim3((unsigned)((po + 255) / 256)), dim3(256), 0, s, tk);
-  }
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
   if (mode == kModeSplit)
@@ -3051,6 +3032,18 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.bin_shift = k.bin_shift;
     sk.nbins = k.nbins;
     sk.scramble = k.scramble;
+    for (int l = 0; l <= 16; ++l) sk.tv_off[l] = 0;
+    sk.g_tv = a->g_tv;
+    if (tv_rec) {
+      sk.tv = tvk;
+      int off = 0;
+      for (int l = 0; l < a->tv->n_levels; ++l) {
+        sk.tv_off[l] = off;
+        const int n1 = a->tv->cube[l] + 1;
+        off += (n1 + 1) / 2 * n1 * n1;
+      }
+      for (int l = a->tv->n_levels; l <= 16; ++l) sk.tv_off[l] = off;
+    }
     hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), 0, s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
@@ -3066,8 +3059,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.overwrite = (a->d_table_mode & 1) != 0;
     r.fused = a->table_step != nullptr;
     if (r.fused) r.step = *a->table_step;
-    // one block per producer's overflow list, + the TV list
-    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks + 1), dim3(kPlaceThreads), 0, s, r);
+    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
     if ((st = hip_status(hipGetLastError()))) return st;
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
                        (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
