@@ -1536,6 +1536,12 @@ struct ScK {
 #define HN_SC_PERM 0
 #endif
 constexpr int kScWaves = 16;
+#ifndef HN_SC_LGROUP   // levels per scatter pass (16: all levels per unit at once; 4: level-group major,
+                       // measured slower: scatter 224 -> 264 us, WRITE_SIZE unchanged 613 -> 609 MB)
+#define HN_SC_LGROUP 16
+#endif
+constexpr int kScLG = HN_SC_LGROUP;
+static_assert(kScLG == 4 || kScLG == 8 || kScLG == 16, "level groups of whole tile-order chunks");
 constexpr int kScMaxBinsLog2 = 13;
 constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
 #ifndef HN_BIN_SHIFT_DEFAULT
@@ -1577,6 +1583,13 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int64_t u0 = (int64_t)blockIdx.x * per;
   const int64_t u1 = u0 + per < units ? u0 + per : units;
   const int pp = lane & 15;
+  // Level groups (HN_SC_LGROUP levels each, level-major over the block's
+  // units): a group's records go to its levels' bins only, so at a time each
+  // producer keeps LG / 16 of its bin regions open -- partially written lines
+  // that would leave L2 before they fill (write amplification) -- and the
+  // group's grads are one tile-order chunk pair (LG = 4: chunk g of both lane
+  // halves), so the loads stay the same; only the ray / point are redone.
+  for (int g = 0; g < 16 / kScLG; ++g)
   for (int64_t u = u0 + wave; u < u1; u += kScWaves) {
 #if HN_SC_PERM
     // the block's rays spread over the (spatially ordered) batch: fewer
@@ -1599,18 +1612,20 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     ray_point(r, k.z_fine[ray * kSf + i], pt);
 #pragma unroll
     for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
-    // grads [f][level]: the tile-order chunks of lanes (p, h = 0) and (p, h = 1)
-    float gf[2][16];
+    // grads [f][level - LG g]: tile-order chunks c of lanes (p, h = 0) and (p, h = 1)
+    // (levels 4c .. 4c + 3 live in chunk c: tile_level)
+    constexpr int NC = kScLG / 4;
+    float gf[2][kScLG];
     const f32x4* tb = reinterpret_cast<const f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const f32x4 q = tb[64 * c + 32 * h + (i & 31)];
+      for (int cc = 0; cc < NC; ++cc) {
+        const f32x4 q = tb[64 * (NC * g + cc) + 32 * h + (i & 31)];
         const float e[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int reg = 4 * c + j;
+          const int reg = 4 * cc + j;   // relative to the group's first chunk
           gf[reg & 1][tile_level(reg >> 1, h)] = e[j];
         }
       }
@@ -1620,12 +1635,12 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const f32x4 q = tw[64 * c + 32 * h + (src & 31)];
+        for (int cc = 0; cc < NC; ++cc) {
+          const f32x4 q = tw[64 * (NC * g + cc) + 32 * h + (src & 31)];
           const float e[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int reg = 4 * c + j;
+            const int reg = 4 * cc + j;
             float& d = gf[reg & 1][tile_level(reg >> 1, h)];
             d = d + e[j];
           }
@@ -1634,12 +1649,13 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     {   // non-finite inputs (NaN / Inf in a grad or the point): one sum, one test per lane
       float chk = (pt[0] + pt[1]) + pt[2];
 #pragma unroll
-      for (int l = 0; l < 16; ++l) chk += gf[0][l] + gf[1][l];
+      for (int ll = 0; ll < kScLG; ++ll) chk += gf[0][ll] + gf[1][ll];
       if (__ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
         __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
-    for (int l = 0; l < 16; ++l) {
+    for (int ll = 0; ll < kScLG; ++ll) {
+      const int l = kScLG * g + ll;
       int32_t cell[3];
       float w[3];
 #if HN_SC_FASTCELL
@@ -1655,7 +1671,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       // lane 0 of every row is a head, so these never carry across rows
       const uint64_t nz1 = ~hb & 0xfffefffefffefffeull, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
       const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
-      const float g0 = gf[0][l], g1 = gf[1][l];
+      const float g0 = gf[0][ll], g1 = gf[1][ll];
       const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
       // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
       const float gz[2][2] = {{g0 * az, g1 * az}, {g0 * w[2], g1 * w[2]}};   // [k][f]
