@@ -111,6 +111,103 @@ def allreduce_grads(table, mlp_params, group=None, live=None):
         off += n
 
 
+class ShardedTableStep:
+    """Data-parallel exchange + RAdam step of the hash table as reduce-scatter
+    -> RAdam on this rank's shard -> all-gather (SURVEY 8e's alternative to
+    one all-reduce): the same bytes on the wire as the
+    all-reduce, 1/world of the dense optimizer work per rank (radam.py:28-94
+    over 16.7 M / 134 M parameters).
+
+    The exchanged vector is the table packed as [levels n_lv.. (dense) |
+    the live rows of the coarse levels 0..n_lv-1 (train.live_rows: the rest
+    of those levels is a structural zero on every rank) | zero pad], so the
+    wire carries 40 MB instead of 64 MiB at T=19 / finest 512.  Gradient and
+    parameters each live in one buffer laid out [coarse dense | dense tail |
+    packed coarse | pad]: the render backward writes the table gradient into
+    its first part as usual, and the packed vector is the buffer from the
+    tail on -- contiguous, no copy of the 60 MB tail.  The table parameter is
+    re-pointed into the parameter buffer, so the all-gather (in place) updates
+    the tail directly and the coarse live rows are scattered back (4 MB).
+    The table's RAdam moments exist for this rank's shard only;
+    gather_state() rebuilds the full ones (dead rows: zero, as the dense
+    reference keeps them) for a checkpoint."""
+
+    def __init__(self, table, live, rank, world, group=None):
+        L_, R, F_ = table.shape
+        self.table, self.rank, self.world, self.group = table, rank, world, group
+        self.full = L_ * R * F_
+        n_lv, rows = live if live is not None else (0, None)
+        self.rows = rows
+        self.head = n_lv * R * F_
+        self.nc = 0 if rows is None else rows.numel() * F_
+        n = self.full - self.head + self.nc
+        self.P = (n + world - 1) // world * world
+        self.s = self.P // world
+        dev = table.device
+        self.gbuf = torch.zeros(self.head + self.P, dtype=torch.float32, device=dev)
+        self.pbuf = torch.zeros(self.head + self.P, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            self.pbuf[:self.full].copy_(table.data.reshape(-1))
+        table.data = self.pbuf[:self.full].view(L_, R, F_)
+        self.m = torch.zeros(self.s, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(self.s, dtype=torch.float32, device=dev)
+        self.gloo = dist.get_backend(group) == "gloo"
+
+    def grad_view(self):
+        """Where the render backward writes the table gradient (overwrite)."""
+        return self.gbuf[:self.full].view(self.table.shape)
+
+    def _packed_coarse(self, buf):
+        F_ = self.table.shape[2]
+        return buf[self.full:self.full + self.nc].view(-1, F_)
+
+    @torch.no_grad()
+    def step(self, coeffs):
+        """After the backward: exchange the gradient, RAdam step on the shard
+        (hn_radam_step, the reference's per-element op forms), all-gather."""
+        F_ = self.table.shape[2]
+        if self.nc:
+            torch.index_select(self.gbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.gbuf))
+            torch.index_select(self.pbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.pbuf))
+        packed_g = self.gbuf[self.head:]
+        lo = self.head + self.rank * self.s
+        if self.gloo:      # gloo has no reduce-scatter: the rehearsal all-reduces and slices
+            dist.all_reduce(packed_g, group=self.group)
+            g_shard = self.gbuf[lo:lo + self.s]
+        else:
+            g_shard = torch.empty(self.s, dtype=torch.float32, device=self.gbuf.device)
+            dist.reduce_scatter_tensor(g_shard, packed_g, group=self.group)
+        p_shard = self.pbuf[lo:lo + self.s]
+        HF.radam_step([(p_shard, g_shard, self.m, self.v, coeffs)])
+        if self.gloo:
+            parts = list(self.pbuf[self.head:].chunk(self.world))
+            mine = p_shard.clone()
+            dist.all_gather(parts, mine, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.pbuf[self.head:], p_shard, group=self.group)
+        if self.nc:
+            self.pbuf[:self.head].view(-1, F_).index_copy_(0, self.rows, self._packed_coarse(self.pbuf))
+
+    @torch.no_grad()
+    def gather_state(self):
+        """Full-size (exp_avg, exp_avg_sq) of the table from every rank's shard."""
+        out = []
+        F_ = self.table.shape[2]
+        for sh in (self.m, self.v):
+            packed = torch.empty(self.P, dtype=torch.float32, device=sh.device)
+            if self.gloo:
+                dist.all_gather(list(packed.chunk(self.world)), sh.clone(), group=self.group)
+            else:
+                dist.all_gather_into_tensor(packed, sh, group=self.group)
+            full = torch.zeros(self.full, dtype=torch.float32, device=sh.device)
+            full[self.head:] = packed[:self.full - self.head]
+            if self.nc:
+                full[:self.head].view(-1, F_).index_copy_(0, self.rows,
+                                                          packed[self.full - self.head:][:self.nc].view(-1, F_))
+            out.append(full.view(self.table.shape))
+        return out
+
+
 def default_args(**over):
     """chair.txt + run_nerf.py defaults (configs/chair.txt:1-19, README.md:20)."""
     a = dict(N_rand=1024, N_samples=64, N_importance=128, use_viewdirs=True, white_bkgd=True,
@@ -285,6 +382,10 @@ class Trainer:
         # explicit mode, one GPU: fuse the table's RAdam step into the binned
         # backward's owner pass when the step has no TV term
         self.fuse_table_step = True
+        # explicit mode, world > 1: reduce-scatter / sharded RAdam / all-gather
+        # of the table (ShardedTableStep) instead of all-reduce + full RAdam
+        self.dp_sharded = True
+        self._xchg = None
 
     def _train_image(self):
         """np.random.choice(i_train) (run_nerf.py:578) from the host generator."""
@@ -350,13 +451,26 @@ class Trainer:
         loss = dp_loss(mse, mse0, sp, self.world, a.sparse_loss_weight, tv, a.tv_loss_weight)
         return loss, mse
 
+    def _live_rows(self):
+        if not hasattr(self, "_live"):
+            e = self.embed_fn
+            lv = live_rows(e.resolutions, e.log2_hashmap_size)
+            self._live = None if lv is None else (lv[0], lv[1].to(self.device))
+        return self._live
+
     def allreduce_grads(self):
         if self.world > 1:
-            if not hasattr(self, "_live"):
-                e = self.embed_fn
-                lv = live_rows(e.resolutions, e.log2_hashmap_size)
-                self._live = None if lv is None else (lv[0], lv[1].to(self.device))
-            allreduce_grads(self.embed_fn.table, self.grad_vars, live=self._live)
+            allreduce_grads(self.embed_fn.table, self.grad_vars, live=self._live_rows())
+
+    def sync_optimizer_state(self):
+        """With the sharded table step (world > 1): gather the table's RAdam
+        moments from the ranks' shards into optimizer.state (for a checkpoint,
+        run_nerf.py:663-680).  Collective: call on every rank."""
+        if self._xchg is not None and self.embed_fn.table in self.optimizer.state:
+            m, v = self._xchg.gather_state()
+            st = self.optimizer.state[self.embed_fn.table]
+            st["exp_avg"].copy_(m)
+            st["exp_avg_sq"].copy_(v)
 
     def _fused_setup(self):
         from .render import _fusable, _linspace_cached
@@ -370,7 +484,14 @@ class Trainer:
         self._t_vals = _linspace_cached(kw["N_samples"], self.device)
         self._ws = nf.weights() + nfine.weights()
         table = self.embed_fn.table
-        self._gtable = torch.zeros_like(table)
+        # world > 1 (explicit mode): the table's exchange + RAdam step sharded over
+        # the ranks (ShardedTableStep); the backward writes into its buffer
+        self._xchg = None
+        if self.world > 1 and self.dp_sharded:
+            self._xchg = ShardedTableStep(table, self._live_rows(), self.rank, self.world)
+            self._gtable = self._xchg.grad_view()
+        else:
+            self._gtable = torch.zeros_like(table)
         self._binned = HF.L.lib().hn_render_scatter_mode(self._cfg, a.N_rand) == 2
         self._gws = HF.zeros_like_all(self._ws)
         self._one = torch.ones((), device=self.device)
@@ -477,7 +598,23 @@ class Trainer:
                                                  **self.kw_train)
                 loss, mse = self.loss_fn(rgb, extras, target, i)
             loss.backward()
-        self.allreduce_grads()
+        if self._xchg is not None and self.mode == "explicit":
+            # the table: RAdam state advanced here (take_step), its exchange and
+            # update sharded; the ten MLP gradients all-reduced as one bucket
+            table = self.embed_fn.table
+            _, _, _, coeffs = self.optimizer.take_step(table)
+            mlp = [p for p in self.grad_vars if p.grad is not None]
+            flat = torch.cat([p.grad.reshape(-1) for p in mlp])
+            work = dist.all_reduce(flat, async_op=True)
+            self._xchg.step(coeffs)
+            work.wait()
+            off = 0
+            for p in mlp:
+                p.grad.copy_(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+            table.grad = None
+        else:
+            self.allreduce_grads()
         self.optimizer.step()
         decay_steps = a.lrate_decay * 1000
         new_lr = a.lrate * (0.1 ** (self.global_step / decay_steps))

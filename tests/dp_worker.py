@@ -46,5 +46,38 @@ def main(batch_path, out_path):
     dist.destroy_process_group()
 
 
+def train(out_path, sharded, steps):
+    """`steps` training steps of the explicit trainer on this rank's own draws,
+    the table exchange sharded (reduce-scatter / shard RAdam / all-gather) or
+    all-reduced; rank 0 saves the table, its RAdam moments and the MLP weights."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    dev = torch.device("cuda", 0)
+    data = SyntheticBlender(64, 64, 4, dev, seed=0)
+    args = default_args(N_rand=256, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=4, sparse_loss_weight=1e-3)
+    tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)
+    tr.dp_sharded = sharded
+    for _ in range(steps):
+        tr.step()
+    tr.sync_optimizer_state()
+    torch.cuda.synchronize()
+    from hashnerf_pytorch_amd import _lib
+    _lib.check_device_faults()
+    if rank == 0:
+        t = tr.embed_fn.table
+        st = tr.optimizer.state[t]
+        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+        torch.save({"table": t.detach().cpu(), "m": st["exp_avg"].cpu(), "v": st["exp_avg_sq"].cpu(),
+                    "step": st["step"], "mlp": [p.detach().cpu() for p in ws]}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    if sys.argv[1] == "train":
+        train(sys.argv[2], sys.argv[3] == "1", int(sys.argv[4]))
+    else:
+        main(sys.argv[1], sys.argv[2])

@@ -56,6 +56,46 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
 
 
+def _launch(args, world=2, timeout=150):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dp_worker.py")] + args,
+                                      env=env, cwd=ROOT))
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=timeout))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert codes == [0] * world, codes
+
+
+def test_dp_sharded_table_step_equals_allreduce(hn, tmp_path):
+    """Two ranks, 8 training steps each (RAdam updates from step 6; TV on
+    through step 4): the sharded exchange (reduce-scatter -> RAdam on the
+    rank's shard -> all-gather, train.ShardedTableStep) leaves the table, its
+    gathered RAdam moments and the MLP weights bitwise equal to the all-reduce
+    + full RAdam path (two-rank sums are order-free; the per-element update is
+    the same kernel)."""
+    res = {}
+    for sharded in (1, 0):
+        out = str(tmp_path / f"train_{sharded}.pt")
+        _launch(["train", out, str(sharded), "8"])
+        res[sharded] = torch.load(out, weights_only=True)
+    a, b = res[1], res[0]
+    assert a["step"] == b["step"] == 8
+    for k in ("table", "m", "v"):
+        assert torch.equal(a[k], b[k]), k
+    assert torch.count_nonzero(a["m"]) > 0
+    for x, y in zip(a["mlp"], b["mlp"]):
+        assert torch.equal(x, y)
+
+
 def test_dp_two_ranks_equal_global_batch(hn, tmp_path):
     tr, spec_args = _trainer(hn, 512)
     i = 1
