@@ -1,0 +1,24 @@
+#!/bin/bash
+# Paired PSNR@5k runs (HIP trainer vs the reference path, tests/test_psnr.py)
+# at several seeds IN PARALLEL on the one GPU (the reference path is bound by
+# its eager launches on the host, one core each), then the aggregate with its
+# 95 % CI (scripts/psnr_aggregate.py).
+#   usage: scripts/gpu_psnr_multi.sh TAG SEED0 SEED1 ...
+set -o pipefail
+TAG=$1
+shift
+OUT=gpurun_out/psnr_$TAG
+mkdir -p $OUT
+PIDS=()
+for S in "$@"; do
+  HN_PSNR_SEED=$S HN_PSNR_ITERS=5000 HN_PSNR_EVERY=100 HN_PSNR_RES=200 HN_PSNR_NTRAIN=100 HN_PSNR_NTEST=8 \
+  HN_PSNR_OUT=$OUT/psnr_5k_${TAG}_seed$S.json OMP_NUM_THREADS=1 \
+      timeout -k 10 1080 python -u -m pytest tests/test_psnr.py -q -s -p no:cacheprovider \
+      > $OUT/psnr_5k_${TAG}_seed$S.log 2>&1 &
+  PIDS+=($!)
+done
+RC=0
+for P in "${PIDS[@]}"; do wait $P || RC=$?; done
+echo "runs rc=$RC"
+ls $OUT/*.json > /dev/null 2>&1 && python scripts/psnr_aggregate.py $OUT/psnr_5k_${TAG}.json $OUT/psnr_5k_${TAG}_seed*.json
+exit $RC

@@ -31,8 +31,8 @@ HN_PSNR_NTRAIN=100 HN_PSNR_OUT=path gives one paired run at 5k iterations
 (HN_PSNR_SEED picks its seed) and writes the curve as JSON.  The "@5k" figure
 is the mean over paired seeds, checked against +-0.1 dB by
 scripts/psnr_aggregate.py (scripts/gpu_psnr.sh; profiles/r01/psnr_5k.json):
-one paired run alone is checked against 0.25 dB, since equally good runs at
-different seeds land ~0.15 dB apart.  The short default run is a training
+one paired run alone is checked against 0.5 dB (TOL_DB_RUN), since the paired
+difference of single runs spreads with a standard deviation of ~0.19 dB.  The short default run is a training
 smoke check: mid-climb, paired runs differ by up to ~0.6 dB either way, so it
 is held to TOL_DB_SHORT.
 """
@@ -47,11 +47,17 @@ import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOL_DB = 0.1          # at 5k iterations: the metric's bar, on the mean over paired seeds
-TOL_DB_RUN = 0.25     # one paired run at 5k iterations: two equally good runs land ~0.15 dB apart
-TOL_DB_SHORT = 0.75   # the default 400-iteration run, still climbing ~1 dB / 100 it: over seeds 0-2
-                      # the paired difference measured +0.07 / +0.15 / -0.49 dB (atomic scatter) and
-                      # +0.24 / +0.28 / -0.59 dB (binned scatter) (scripts/psnr_short_ab.sh)
+TOL_DB = 0.1          # at 5k iterations: the metric's bar, on the mean over paired seeds (its 95 %
+                      # confidence interval, scripts/psnr_aggregate.py)
+TOL_DB_RUN = 0.5      # one paired run at 5k iterations: a sanity bound, not the metric -- the paired
+                      # difference of single runs has a standard deviation of ~0.19 dB (six seeds,
+                      # round 2), so 0.5 dB is ~2.6 sigma; the 0.1 dB bar is carried by the mean
+TOL_DB_SHORT = 0.75   # the default 400-iteration run, still climbing ~1 dB / 100 it: paired runs
+                      # differ by up to ~0.6 dB either way (scripts/psnr_short_ab.sh), so this run's
+                      # gate is the absolute floor below; the band only catches a gross regression
+FLOOR_DB_SHORT = 13.0  # the short run's HIP PSNR must clear this: the untrained (all-white)
+                       # prediction scores 9.07 dB on its 4 test views, the HIP path 15.09 dB
+                       # after 400 iterations (r03e)
 
 
 def _oracle_trainer(O, tr, dev):
@@ -119,7 +125,8 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     H = W = int(os.environ.get("HN_PSNR_RES", "100"))
     n_train = int(os.environ.get("HN_PSNR_NTRAIN", "50"))
     args = default_args(N_rand=1024, H=H, W=W, n_train=n_train)
-    data = SyntheticBlender(H, W, n_train, DEV, scene="procedural", n_test=4)
+    n_test = int(os.environ.get("HN_PSNR_NTEST", "4"))
+    data = SyntheticBlender(H, W, n_train, DEV, scene="procedural", n_test=n_test)
     seed = int(os.environ.get("HN_PSNR_SEED", "0"))
     tr = Trainer(args, data, DEV, seed=seed)
     box = tuple(torch.as_tensor(t, dtype=torch.float32).to(DEV) for t in data.bounding_box)
@@ -156,6 +163,9 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     stat = dict(psnr_hip=med("psnr_hip"), psnr_ref=med("psnr_ref"), n_evals=len(tail),
                 from_iter=tail[0]["iter"], mean_hip=mean("psnr_hip"), mean_ref=mean("psnr_ref"))
     stat["diff"] = round(stat["psnr_hip"] - stat["psnr_ref"], 4)
+    # the lower-variance statistic the multi-seed aggregate uses: the mean over
+    # the tail evaluations of the paired (same-iteration) differences
+    stat["diff_mean"] = mean("diff")
     # scale of the bar: the HIP path alone at other seeds (other images,
     # pixels, jitter and init) -- how far two equally good runs land apart
     seeds = int(os.environ.get("HN_PSNR_SEEDS", "0"))
@@ -171,7 +181,7 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     if spread:
         stat["hip_other_seeds"] = spread
     tol = TOL_DB_RUN if iters >= 5000 else TOL_DB_SHORT
-    out = dict(iters=iters, seed=seed, H=H, W=W, N_rand=args.N_rand, n_train=n_train, n_test=4,
+    out = dict(iters=iters, seed=seed, H=H, W=W, N_rand=args.N_rand, n_train=n_train, n_test=n_test,
                scene="procedural chair (train.procedural_field)", tol_db=tol, final=stat, curve=curve,
                ms_per_iter_hip=round(1e3 * t_hip / iters, 3),
                ms_per_iter_ref_eager_gpu=round(1e3 * t_ref / iters, 3))
@@ -181,5 +191,5 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         with open(path, "w") as f:
             json.dump(out, f, indent=1)
-    assert stat["psnr_hip"] > 12.0, "the HIP path did not learn the scene"
-    assert abs(stat["diff"]) <= tol, out
+    assert stat["psnr_hip"] > (FLOOR_DB_SHORT if iters < 5000 else 12.0), "the HIP path did not learn the scene"
+    assert abs(stat["diff_mean"]) <= tol, out
