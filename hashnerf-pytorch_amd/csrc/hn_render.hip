@@ -617,6 +617,24 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
   return a;
 }
 
+// HN_B1_SWP 1: the next chunk's B split (VALU) is issued in the gaps of this
+// chunk's MFMAs (sched_group_barrier: one MFMA, then V VALU) instead of after
+// them; the same splits and the same MFMA order, so results are unchanged.
+// Measured (r03g, config 2, two runs each on one box): backward launch
+// 0.812 -> 0.789 ms, step 1.159 -> 1.134 ms; the kernel's 24 VGPR spills go to 0.
+// The same pipelining in the forward's gemm (HN_GEMM_SWP, hn_mlp.h) changed
+// nothing there (render_fwd 0.304 ms either way).
+#ifndef HN_B1_SWP
+#define HN_B1_SWP 1
+#endif
+template <int NMFMA, int NVALU>
+HN_DEV void swp_pattern() {
+  static_for<0, NMFMA>([&](auto) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // one MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, NVALU, 0);   // then VALU
+  });
+}
+
 // acc += A(segment SEG of the stream) . B, bval(s) = B operand of f32 k-step s.
 // IMG >= 0: chunk c's first two B parts also go to image tile IMG + c / 2 at
 // quad offset F4B + 4 (c % 2) (put_parts; Xb = the wave's images).
@@ -624,7 +642,26 @@ template <int SEG, int IMG = -1, int F4B = 0, typename BF>
 HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, char* Xb = nullptr) {
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
-  if constexpr (NS > 0) {                       // split-f32: NS groups per K = 16 chunk
+  if constexpr (NS > 0 && HN_B1_SWP && KS > 8) {   // split-f32, next chunk's split in the MFMA gaps
+    constexpr int NC = KS / 8;
+    SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, NC>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      SP<NS> a;
+      static_for<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        a.p[q] = as_bf16x8(wring_take<START + NS * c + q>(w, P, lane));
+      });
+      if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
+      acc = mfma_split<NS>(a, b, acc);
+      if constexpr (c + 1 < NC) {
+        b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
+        swp_pattern<NS == 3 ? 6 : 3, NS == 3 ? 6 : 7>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  } else if constexpr (NS > 0) {                // split-f32: NS groups per K = 16 chunk
     static_for<0, KS / 8>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
       SP<NS> a;
@@ -656,7 +693,30 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(kSegs[SEG].ob < 0, "paired segment");
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
-  if constexpr (NS > 0) {
+  if constexpr (NS > 0 && HN_B1_SWP && KS > 8) {
+    constexpr int NC = KS / 8;
+    SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, NC>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      SP<NS> a0, a1;
+      static_for<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        a0.p[q] = as_bf16x8(wring_take<START + 2 * NS * c + q>(w, P, lane));
+      });
+      static_for<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        a1.p[q] = as_bf16x8(wring_take<START + 2 * NS * c + NS + q>(w, P, lane));
+      });
+      if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
+      mfma_split2<NS>(a0, a1, b, acc0, acc1);
+      if constexpr (c + 1 < NC) {
+        b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
+        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : 4>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  } else if constexpr (NS > 0) {
     constexpr int NC = KS / 8;
     static_for<0, NC>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
@@ -742,6 +802,24 @@ HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
   }
 }
 
+// Ordering of a wave's own LDS image writes and transposed reads inside a
+// tile.  The LDS unit executes one wave's ds instructions in order, so a read
+// issued after a write sees it (also another lane's) and a write after a read
+// does not overwrite what the read returns: only the compiler must keep the
+// program order (HN_B1_LDS_ORDER 1: a compiler barrier; the reads' own
+// lgkmcnt waits stay).  0: s_waitcnt lgkmcnt(0) at each hand-over
+// (lds_fence_wave), which also waits for every write still in flight.
+#ifndef HN_B1_LDS_ORDER
+#define HN_B1_LDS_ORDER 1
+#endif
+HN_DEV void tile_lds_order() {
+#if HN_B1_LDS_ORDER
+  asm volatile("" ::: "memory");
+#else
+  lds_fence_wave();
+#endif
+}
+
 // color_net.0 applied to the ray's sh features (the same for every point of
 // the ray): HN_C0SH_LDS 1 keeps its 64 rows in the wave's LDS slab after the
 // images (read back as the c0 accumulators' seed, 8 broadcast ds_read_b128
@@ -817,7 +895,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     }
   }
   after_fwd();
-  lds_fence_wave();
+  tile_lds_order();
   // ---- color_net.2 (dW rows >= 3 are discarded) ----
   {
     const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
@@ -833,7 +911,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   gemm2<R_B3, kBC1>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; }, Xb);
   mask_bits(dc0[0], mc0, 0);
   mask_bits(dc0[1], mc0, 1);
-  lds_fence_wave();
+  tile_lds_order();
   {
     const int ab[2] = {kBC1, kBC1 + 1}, bb[2] = {kBC0, kBC0 + 1};
     wgrad_n<2, 2>(Xb, ab, bb, dw.c1, lane);     // dw.c1[2 * nb + kb]
@@ -841,7 +919,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   // ---- color_net.0 (dc0 image over c0; B = [sh16 | sigma | geo15]) ----
   f32x16 ds1 = gemm_w<seg_of(R_B2G), kBC0>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; }, Xb);
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
-  lds_fence_wave();
+  tile_lds_order();
   {
     const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBC0in};
     wgrad_n<2, 1>(Xb, ab, bb, dw.c0, lane);
@@ -851,7 +929,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   gemm2<R_B1, kBC1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; }, Xb);
   mask_bits(dh0[0], mh0, 0);
   mask_bits(dh0[1], mh0, 1);
-  lds_fence_wave();
+  tile_lds_order();
   {
     const int ab[1] = {kBC1}, bb[2] = {kBH0, kBH0 + 1};
     wgrad_n<1, 2>(Xb, ab, bb, dw.s1, lane);
@@ -859,7 +937,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   // ---- sigma_net.0 (dh0 image over dc0) ----
   const f32x16 dfeat =
       gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; }, Xb);
-  lds_fence_wave();
+  tile_lds_order();
   {
     const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBF};
     wgrad_n<2, 1>(Xb, ab, bb, dw.s0, lane);
@@ -867,7 +945,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   static_for<kTileGroups, kTilePeriod - kTileGroups>([&](auto gc) {   // pad groups: keep the ring
     (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
   });
-  lds_fence_wave();                             // image reads done before any later writes
+  tile_lds_order();                             // image reads done before any later writes
   return dfeat;
 }
 
@@ -1549,6 +1627,38 @@ constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <=
 #endif
 constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per bin (bin_geom)
 
+// HN_SC_STAGE 1: level-major phases across the block's waves (all 16 waves
+// take level l of their units, then the block syncs), each head lane's record
+// put into an LDS pool at (bin of the level, slot - the bin's first slot of the
+// phase) and the pool flushed by the block in slot order: a bin's records of
+// the phase leave as contiguous runs (one 16-B value and one word per lane,
+// consecutive lanes on consecutive slots) instead of 64 scattered 16-B and 4-B
+// stores per instruction.  Records past the pool's share of their bin (2^kStLog2
+// records over the level's bins) or past the region's capacity are stored
+// directly.  The slot of every record is the same as without staging, so the
+// record buffer, and the owner's sums, are identical.  Measured (r03g, config
+// 2): WRITE_SIZE 548 -> 395 MB per launch for 352 MB of records (1.56x ->
+// 1.12x), backward launch time unchanged (0.813 / 0.814 vs 0.813 / 0.812 ms):
+// the scatter waits on its own dependency chains (SQ_WAIT_INST_ANY 44% of its
+// wave cycles), not on the write traffic.
+#ifndef HN_SC_STAGE
+#define HN_SC_STAGE 1
+#endif
+constexpr int kStLog2 = 12, kStPool = 1 << kStLog2;   // 64 KiB of values + 16 KiB of words
+constexpr int kStMinLog2C = 3;                          // fewer than 8 records per bin: no staging
+struct StPhase {
+  int b0, log2c;   // first bin of the level, log2 pool records per bin (< kStMinLog2C: direct)
+  int nbl;         // bins of the level
+};
+HN_DEV StPhase st_phase(int l, int log2T, int shift) {
+  StPhase ph;
+  ph.b0 = (int)(((uint32_t)l << log2T) >> shift);
+  const int lg = log2T > shift ? log2T - shift : 0;
+  ph.nbl = 1 << lg;
+  ph.log2c = kStLog2 - lg;
+  return ph;
+}
+
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __shared__ uint32_t bcnt[kScMaxBins];
   __shared__ float gsl[kGsLds], lvmx[16];
@@ -1583,6 +1693,42 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int64_t u0 = (int64_t)blockIdx.x * per;
   const int64_t u1 = u0 + per < units ? u0 + per : units;
   const int pp = lane & 15;
+#if HN_SC_STAGE
+  static_assert(kScLG == 16, "staged phases run all levels of a unit");
+  __shared__ f32x4 stv[kStPool];
+  __shared__ uint32_t stw[kStPool];
+  __shared__ uint32_t stfl[2][kStPool >> kStMinLog2C];   // per phase parity: first staged slot per bin
+  const int log2T = (int)k.g.log2T, sh = k.bin_shift;
+  // first staged slot of each bin of level l (the bins' counts so far, capped)
+  auto st_init = [&](int l) {
+    const StPhase ph = st_phase(l, log2T, sh);
+    if (ph.log2c < kStMinLog2C) return;
+    for (int i = threadIdx.x; i < ph.nbl; i += blockDim.x) stfl[l & 1][i] = min(bcnt[ph.b0 + i], bw.cap);
+  };
+  // the pool's records of level l to their regions, in slot order
+  auto st_flush = [&](int l) {
+    const StPhase ph = st_phase(l, log2T, sh);
+    if (ph.log2c < kStMinLog2C) return;
+    const uint32_t c = 1u << ph.log2c;
+    for (int p = threadIdx.x; p < kStPool; p += blockDim.x) {
+      const int bl = p >> ph.log2c, b = ph.b0 + bl;
+      const uint32_t j = (uint32_t)p & (c - 1u), f = stfl[l & 1][bl];
+      const uint32_t end = min(min(bcnt[b], bw.cap), f + c);
+      if (f + j < end) {
+        const size_t r = bw.base + (size_t)b * bw.stride + f + j;
+        *reinterpret_cast<f32x4*>(bw.bins + rec_vofs(r)) = stv[p];
+        reinterpret_cast<uint32_t*>(bw.bins)[rec_wofs(r, bw.nrec)] = stw[p];
+      }
+    }
+  };
+  st_init(0);
+  __syncthreads();
+  const int64_t n_it = (u1 - u0 + kScWaves - 1) / kScWaves;   // the same for every wave of the block
+  constexpr int g = 0;
+  for (int64_t it = 0; it < n_it; ++it) {
+    const int64_t u = u0 + wave + it * kScWaves;
+    const bool act = u < u1;
+#else
   // Level groups (HN_SC_LGROUP levels each, level-major over the block's
   // units): a group's records go to its levels' bins only, so at a time each
   // producer keeps LG / 16 of its bin regions open -- partially written lines
@@ -1591,6 +1737,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // halves), so the loads stay the same; only the ray / point are redone.
   for (int g = 0; g < 16 / kScLG; ++g)
   for (int64_t u = u0 + wave; u < u1; u += kScWaves) {
+    constexpr bool act = true;
+#endif
 #if HN_SC_PERM
     // the block's rays spread over the (spatially ordered) batch: fewer
     // same-entry records per region at the coarse levels
@@ -1607,15 +1755,16 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 #endif
     const int i = 64 * (int)(u % 3) + lane;       // fine sample
     Ray r;
-    load_ray(k.rays, ray, r);
     float pt[3], xc[3];
+    float gf[2][kScLG];
+    if (act) {
+    load_ray(k.rays, ray, r);
     ray_point(r, k.z_fine[ray * kSf + i], pt);
 #pragma unroll
     for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
     // grads [f][level - LG g]: tile-order chunks c of lanes (p, h = 0) and (p, h = 1)
     // (levels 4c .. 4c + 3 live in chunk c: tile_level)
     constexpr int NC = kScLG / 4;
-    float gf[2][kScLG];
     const f32x4* tb = reinterpret_cast<const f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -1653,9 +1802,15 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       if (__ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
         __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    }   // act
 #pragma unroll
     for (int ll = 0; ll < kScLG; ++ll) {
       const int l = kScLG * g + ll;
+#if HN_SC_STAGE
+      const StPhase ph = st_phase(l, log2T, sh);
+      const bool staged = ph.log2c >= kStMinLog2C;
+#endif
+      if (act) {
       int32_t cell[3];
       float w[3];
 #if HN_SC_FASTCELL
@@ -1692,7 +1847,18 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       }
       if (HN_SC_BATCH && head) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) rec_store(bw, rs[c], v[c]);
+        for (int c = 0; c < 4; ++c) {
+#if HN_SC_STAGE
+          const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[l & 1][staged ? bl : 0];
+          if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
+            const int q = (int)((bl << ph.log2c) + j);
+            stv[q] = f32x4{v[c][0], v[c][1], v[c][2], v[c][3]};
+            stw[q] = rs[c].word;
+            continue;
+          }
+#endif
+          rec_store(bw, rs[c], v[c]);
+        }
       }
 #if HN_SC_LANEMAX   // per-lane maxima in LDS (one conflict-free ds_max per level), reduced once per block
       __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
@@ -1702,6 +1868,13 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       if (lane == 0)
         __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+      }   // act
+#if HN_SC_STAGE
+      __syncthreads();   // the phase's records are in the pool, its counts final
+      st_flush(l);
+      st_init(l + 1 < 16 ? l + 1 : 0);   // the next phase's bins (other parity), counts unchanged by the flush
+      __syncthreads();   // the pool is free again
 #endif
     }
   }
