@@ -484,6 +484,9 @@ HN_DEV bf16x8 img_operand(const char* Xb, int blk, int q, int cc, int lane) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+#ifndef HN_WG_SB   // 0: no scheduling barrier after a weight-gradient chunk (the scheduler may mix it with the next GEMM)
+#define HN_WG_SB 0
+#endif
 // acc[NB * a + b] += sum over the tile's 32 points of A(ablk[a]) B(bblk[b])^T
 // (two K = 16 chunks, 2-part products in mfma_split's order)
 template <int NA, int NB>
@@ -503,7 +506,9 @@ HN_DEV void wgrad_n(const char* Xb, const int (&ablk)[NA], const int (&bblk)[NB]
     for (int ja = 0; ja < NA; ++ja)
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = mfma_split<2>(a[ja], b[jb], acc[NB * ja + jb]);
+#if HN_WG_SB
     __builtin_amdgcn_sched_barrier(0);
+#endif
   }
 }
 
@@ -627,6 +632,12 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
 #ifndef HN_B1_SWP
 #define HN_B1_SWP 1
 #endif
+#ifndef HN_SWP_V3   // VALU per MFMA gap, paired 3-part chunk (12 MFMAs; its split is ~36 VALU)
+#define HN_SWP_V3 3
+#endif
+#ifndef HN_SWP_V2   // VALU per MFMA gap, paired 2-part chunk (6 MFMAs; ~20 VALU)
+#define HN_SWP_V2 4
+#endif
 template <int NMFMA, int NVALU>
 HN_DEV void swp_pattern() {
   static_for<0, NMFMA>([&](auto) {
@@ -712,7 +723,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : 4>();
+        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? HN_SWP_V3 : HN_SWP_V2>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -776,13 +787,20 @@ HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, ch
 #ifndef HN_MASK_INT
 #define HN_MASK_INT 1
 #endif
+#ifndef HN_MASK_MIN
+#define HN_MASK_MIN 0
+#endif
 HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
 #if HN_MASK_INT
     const uint32_t b = __float_as_uint(v[r]);
     const uint32_t u = b & ~(uint32_t)((int32_t)b >> 31);
+#if HN_MASK_MIN   // bit = min(u, 1): v_min_u32 + v_lshl_or_b32 per element
+    m |= min(u, 1u) << (16 * ob + r);
+#else
     m |= ((u + 0x7fffffffu) >> 31) << (16 * ob + r);
+#endif
     v[r] = __uint_as_float(u);
 #else
     m |= (v[r] > 0.f ? 1u : 0u) << (16 * ob + r);
@@ -858,10 +876,17 @@ HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
 // after_fwd(): called once the forward recompute is done (its activations
 // live on only as LDS images and mask bits) -- where the next unit's prefetch
 // adds the fewest live registers.
+#ifndef HN_B1_LANE_OPAQUE   // 0: the image addresses may be kept across tiles (registers permitting)
+#define HN_B1_LANE_OPAQUE 1
+#endif
 template <typename AfterFwd>
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
                       const C0Sh& c0sh, float4 dr, DW& dw, AfterFwd&& after_fwd) {
+#if HN_B1_LANE_OPAQUE
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
+#else
+  const int lane = (int)__lane_id();
+#endif
   const int h = lane >> 5;
   char* Xb = reinterpret_cast<char*>(X);
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
