@@ -22,7 +22,12 @@ run_batch() {
         > $OUT/psnr_5k_${TAG}_seed$S.log 2>&1 &
     PIDS+=($!)
   done
+  # heartbeat: the runs print every 500 iterations only (gpurun takes 180 s
+  # without output for a hang)
+  ( while true; do sleep 60; echo "[$(date +%T)] $(tail -qn1 $OUT/psnr_5k_${TAG}_seed$1.log 2>/dev/null | cut -c1-80)"; done ) &
+  local HB=$!
   for P in "${PIDS[@]}"; do wait $P || RC=$?; done
+  kill $HB 2>/dev/null
 }
 SEEDS=("$@")
 for ((i = 0; i < ${#SEEDS[@]}; i += PAR)); do
