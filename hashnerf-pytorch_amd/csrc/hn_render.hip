@@ -788,7 +788,7 @@ HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, ch
 #define HN_MASK_INT 1
 #endif
 #ifndef HN_MASK_MIN
-#define HN_MASK_MIN 0
+#define HN_MASK_MIN 1
 #endif
 HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
@@ -876,6 +876,21 @@ HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
 // after_fwd(): called once the forward recompute is done (its activations
 // live on only as LDS images and mask bits) -- where the next unit's prefetch
 // adds the fewest live registers.
+// HN_TILE_PROF (diagnostic, with HN_PROFILE): shader-clock cycles of the
+// tile's segments summed over all tiles (lane 0 of each wave; the stamps cost
+// ~10 % themselves): [0] F0 [1] F1 + F2G [2] F3 + c1 image [3] dW c2 + B4 [4] B3
+// + dW c1 [5] B2G + dW c0 [6] B1 + dW s1 [7] B0 + dW s0
+#ifndef HN_TILE_PROF
+#define HN_TILE_PROF 0
+#endif
+#if HN_TILE_PROF
+__device__ unsigned long long g_tile[9];
+#define HN_TSTAMP(i) do { __builtin_amdgcn_sched_barrier(0); const uint64_t n_ = __builtin_amdgcn_s_memtime(); \
+    if (i >= 0 && lane == 0) atomicAdd(&g_tile[(i) < 0 ? 8 : (i)], (unsigned long long)(n_ - t_ts)); t_ts = n_; \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define HN_TSTAMP(i) ((void)0)
+#endif
 #ifndef HN_B1_LANE_OPAQUE   // 0: the image addresses may be kept across tiles (registers permitting)
 #define HN_B1_LANE_OPAQUE 1
 #endif
@@ -890,12 +905,17 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   const int h = lane >> 5;
   char* Xb = reinterpret_cast<char*>(X);
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
+#if HN_TILE_PROF
+  uint64_t t_ts = 0;
+  HN_TSTAMP(-1);
+#endif
   // ---- forward recompute (models.py:151-174); each GEMM stages its B
   // operand's parts as a dW operand image ----
   f32x16 h0[2] = {zero16(), zero16()};
   gemm2<R_F0, kBF>(wr, P, h0, lane, [&](int s) { return feat[s]; }, Xb);
   relu_bits(h0[0], mh0, 0);
   relu_bits(h0[1], mh0, 1);
+  HN_TSTAMP(0);
   const f32x16 s1 = gemm_w<seg_of(R_F1), kBH0>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; }, Xb);
   f32x16 c0[2];
   c0sh_seed(c0sh, c0, h);
@@ -903,6 +923,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   gemm2<R_F2G, kBC0in, 4>(wr, P, c0, lane, [&](int s) { return s1[s]; }, Xb);
   relu_bits(c0[0], mc0, 0);
   relu_bits(c0[1], mc0, 1);
+  HN_TSTAMP(1);
   {
     f32x16 c1[2] = {zero16(), zero16()};
     gemm2<R_F3, kBC0>(wr, P, c1, lane, [&](int s) { return c0[s >> 4][s & 15]; }, Xb);
@@ -921,6 +942,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   }
   after_fwd();
   tile_lds_order();
+  HN_TSTAMP(2);
   // ---- color_net.2 (dW rows >= 3 are discarded) ----
   {
     const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
@@ -931,6 +953,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   gemm2<R_B4>(wr, P, dc1, lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
   mask_bits(dc1[0], mc1, 0);
   mask_bits(dc1[1], mc1, 1);
+  HN_TSTAMP(3);
   // ---- color_net.1 (dc1 image over c1) ----
   f32x16 dc0[2] = {zero16(), zero16()};
   gemm2<R_B3, kBC1>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; }, Xb);
@@ -941,6 +964,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     const int ab[2] = {kBC1, kBC1 + 1}, bb[2] = {kBC0, kBC0 + 1};
     wgrad_n<2, 2>(Xb, ab, bb, dw.c1, lane);     // dw.c1[2 * nb + kb]
   }
+  HN_TSTAMP(4);
   // ---- color_net.0 (dc0 image over c0; B = [sh16 | sigma | geo15]) ----
   f32x16 ds1 = gemm_w<seg_of(R_B2G), kBC0>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; }, Xb);
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
@@ -949,6 +973,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBC0in};
     wgrad_n<2, 1>(Xb, ab, bb, dw.c0, lane);
   }
+  HN_TSTAMP(5);
   // ---- sigma_net.1 (ds1 image over dc1's first tile; rows 16..31 discarded) ----
   f32x16 dh0[2] = {zero16(), zero16()};
   gemm2<R_B1, kBC1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; }, Xb);
@@ -959,6 +984,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     const int ab[1] = {kBC1}, bb[2] = {kBH0, kBH0 + 1};
     wgrad_n<1, 2>(Xb, ab, bb, dw.s1, lane);
   }
+  HN_TSTAMP(6);
   // ---- sigma_net.0 (dh0 image over dc0) ----
   const f32x16 dfeat =
       gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; }, Xb);
@@ -971,6 +997,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
   });
   tile_lds_order();                             // image reads done before any later writes
+  HN_TSTAMP(7);
   return dfeat;
 }
 
@@ -3309,6 +3336,16 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
             rg[2] / (256. * kMW), rg[3] / (256. * kMW));
     memset(rg, 0, sizeof(rg));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ring), rg, sizeof(rg));
+#if HN_TILE_PROF
+    unsigned long long tp[9];
+    (void)hipMemcpyFromSymbol(tp, HIP_SYMBOL(g_tile), sizeof(tp));
+    const double ntile = (double)a->n_rays * 8;   // 2 coarse + 6 fine tiles per ray
+    fprintf(stderr, "hn_b1_tile cycles/tile: F0 %.0f F1+F2G %.0f F3 %.0f dWc2+B4 %.0f B3+dWc1 %.0f "
+            "B2G+dWc0 %.0f B1+dWs1 %.0f B0+dWs0 %.0f\n", tp[0] / ntile, tp[1] / ntile, tp[2] / ntile,
+            tp[3] / ntile, tp[4] / ntile, tp[5] / ntile, tp[6] / ntile, tp[7] / ntile);
+    memset(tp, 0, sizeof(tp));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile), tp, sizeof(tp));
+#endif
   }
 #endif
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,

@@ -13,4 +13,4 @@ build.build_variant(["-DHN_PROFILE=1"] + os.environ.get("PROFILE_DEFS", "").spli
 PY
 HN_LIB_PATH=/tmp/hn_profile.so timeout -k 10 300 python bench.py --steps 4 --warmup 2 --no-cpu-baseline "$@" \
     > $OUT/b1_profile.json 2> $OUT/b1_profile.err || exit 1
-grep 'hn_b1_\|hn_fwd_' $OUT/b1_profile.err | tail -8
+grep "hn_b1_\|hn_fwd_" $OUT/b1_profile.err | tail -8

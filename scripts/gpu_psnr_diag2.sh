@@ -3,7 +3,7 @@
 # 5k run's shape) with K of them at once on the one GPU.
 set -o pipefail
 OUT=gpurun_out/psnr_diag; mkdir -p $OUT
-for K in 3 6; do
+for K in ${@:-3 6}; do
   PIDS=()
   for S in $(seq 1 $K); do
     HN_PSNR_SEED=$S HN_PSNR_ITERS=300 HN_PSNR_EVERY=100 HN_PSNR_RES=200 HN_PSNR_NTRAIN=100 HN_PSNR_NTEST=8 \

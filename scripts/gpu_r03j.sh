@@ -22,4 +22,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 python3 scripts/trace_tail_stats.py $OUT/prof_$TAG/prof_kernel_trace.csv 10 > $OUT/prof_$TAG/prof_kernel_stats_timed.csv
 rm -f $OUT/prof_$TAG/prof_kernel_trace.csv
 head -6 $OUT/prof_$TAG/prof_kernel_stats_timed.csv | cut -c1-110
+HN_LIB_PATH=hashnerf-pytorch_amd/build/var_tileprof.so timeout -k 10 300 python bench.py --steps 4 --warmup 2 --no-cpu-baseline \
+    > $OUT/tileprof_$TAG.json 2> $OUT/tileprof_$TAG.err || exit 7
+grep "hn_b1_" $OUT/tileprof_$TAG.err | tail -4
+timeout -k 10 400 bash scripts/gpu_psnr_diag2.sh 3 || exit 8
 echo "chain ok"
