@@ -1665,6 +1665,9 @@ struct ScK {
 #ifndef HN_SC_PERM       // 1: a block's rays through the backward's batch permutation
 #define HN_SC_PERM 0
 #endif
+#ifndef HN_SC_ROLL   // 1: levels in a rolled loop of level pairs (one copy of the level code)
+#define HN_SC_ROLL 0
+#endif
 constexpr int kScWaves = 16;
 #ifndef HN_SC_LGROUP   // levels per scatter pass (16: all levels per unit at once; 4: level-group major,
                        // measured slower: scatter 224 -> 264 us, WRITE_SIZE unchanged 613 -> 609 MB)
@@ -1776,7 +1779,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   st_init(0);
   __syncthreads();
   const int64_t n_it = (u1 - u0 + kScWaves - 1) / kScWaves;   // the same for every wave of the block
-  constexpr int g = 0;
+  [[maybe_unused]] constexpr int g = 0;
   for (int64_t it = 0; it < n_it; ++it) {
     const int64_t u = u0 + wave + it * kScWaves;
     const bool act = u < u1;
@@ -1808,6 +1811,118 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     const int i = 64 * (int)(u % 3) + lane;       // fine sample
     Ray r;
     float pt[3], xc[3];
+    // one level of the unit: voxel, run heads, the 4 corner rows' records
+    auto level = [&](const int l, const float g0, const float g1) {
+#if HN_SC_STAGE
+        const StPhase ph = st_phase(l, log2T, sh);
+        const bool staged = ph.log2c >= kStMinLog2C;
+#endif
+        if (act) {
+        int32_t cell[3];
+        float w[3];
+#if HN_SC_FASTCELL
+        voxel_cw_sc(k.g, gsl, pt, xc, l, cell, w);
+#else
+        voxel_cw(k.g, gsl, pt, xc, l, cell, w);
+#endif
+        const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
+        const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
+        const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
+        const uint64_t hb = __ballot(head);
+        const uint32_t pm = (uint32_t)(hb >> (lane & 48)) & 0xffffu;
+        // lane 0 of every row is a head, so these never carry across rows
+        const uint64_t nz1 = ~hb & 0xfffefffefffefffeull, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
+        const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
+      
+        const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
+        // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
+        const float gz[2][2] = {{g0 * az, g1 * az}, {g0 * w[2], g1 * w[2]}};   // [k][f]
+        float vmax = 0.f;   // largest |record value| of the level: the owner's fixed-point scale
+        float v[4][4];
+        RecSlot rs[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {   // sums and slots of the 4 corner rows: 4 counter round trips in flight
+          const int j = c >> 1, kk = c & 1;
+          const float wy = j ? w[1] : ay;
+          const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
+          v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
+          seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
+          vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+          if (head) rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)k.g.log2T, cx, j ? y0 + kPrimeY : y0,
+                                     kk ? z0 + kPrimeZ : z0);
+          if (!HN_SC_BATCH && head) rec_store(bw, rs[c], v[c]);
+        }
+        if (HN_SC_BATCH && head) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+#if HN_SC_STAGE
+            const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[l & 1][staged ? bl : 0];
+            if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
+              const int q = (int)((bl << ph.log2c) + j);
+              stv[q] = f32x4{v[c][0], v[c][1], v[c][2], v[c][3]};
+              stw[q] = rs[c].word;
+              continue;
+            }
+#endif
+            rec_store(bw, rs[c], v[c]);
+          }
+        }
+#if HN_SC_LANEMAX   // per-lane maxima in LDS (one conflict-free ds_max per level), reduced once per block
+        __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+        vmax = wave_max_f32(vmax);
+        if (lane == 0)
+          __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+        }   // act
+#if HN_SC_STAGE
+      __syncthreads();   // the phase's records are in the pool, its counts final
+      st_flush(l);
+      st_init(l + 1 < 16 ? l + 1 : 0);   // the next phase's bins (other parity), counts unchanged by the flush
+      __syncthreads();   // the pool is free again
+#endif
+    };
+#if HN_SC_ROLL
+    // grads loaded per level pair inside a rolled loop (one copy of the level
+    // code for two levels instead of sixteen: the unrolled kernel was 84 KB,
+    // over the 64 KB instruction cache two CUs share)
+    static_assert(kScLG == 16, "rolled levels: all levels of a unit");
+    const f32x4* tb = nullptr;
+    const f32x4* tw = nullptr;
+    int src = kSc;
+    float chk = 0.f;
+    if (act) {
+      load_ray(k.rays, ray, r);
+      ray_point(r, k.z_fine[ray * kSf + i], pt);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
+      tb = reinterpret_cast<const f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024);
+      src = k.fine_src[ray * kSf + i];
+      if (src < kSc) tw = reinterpret_cast<const f32x4*>(k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024);
+      chk = (pt[0] + pt[1]) + pt[2];
+    }
+    // level pair lp = levels 2 lp, 2 lp + 1 = chunk lp / 2 of lane half lp % 2
+    // (tile_level): elements (f0, f1) of the lower level, then of the upper
+#pragma clang loop unroll(disable)
+    for (int lp = 0; lp < 8; ++lp) {
+      f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (act) {
+        q = tb[64 * (lp >> 1) + 32 * (lp & 1) + (i & 31)];
+        if (src < kSc) {                          // coarse twin: fine + coarse grads
+          const f32x4 e = tw[64 * (lp >> 1) + 32 * (lp & 1) + (src & 31)];
+          q = f32x4{q.x + e.x, q.y + e.y, q.z + e.z, q.w + e.w};
+        }
+        chk += (q.x + q.y) + (q.z + q.w);
+      }
+      level(2 * lp, q.x, q.y);
+      level(2 * lp + 1, q.z, q.w);
+    }
+    // non-finite inputs (NaN / Inf in a grad or the point): one test per lane
+    if (act && __ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
+      __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
     float gf[2][kScLG];
     if (act) {
     load_ray(k.rays, ray, r);
@@ -1856,79 +1971,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     }
     }   // act
 #pragma unroll
-    for (int ll = 0; ll < kScLG; ++ll) {
-      const int l = kScLG * g + ll;
-#if HN_SC_STAGE
-      const StPhase ph = st_phase(l, log2T, sh);
-      const bool staged = ph.log2c >= kStMinLog2C;
+    for (int ll = 0; ll < kScLG; ++ll) level(kScLG * g + ll, gf[0][ll], gf[1][ll]);
 #endif
-      if (act) {
-      int32_t cell[3];
-      float w[3];
-#if HN_SC_FASTCELL
-      voxel_cw_sc(k.g, gsl, pt, xc, l, cell, w);
-#else
-      voxel_cw(k.g, gsl, pt, xc, l, cell, w);
-#endif
-      const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
-      const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
-      const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
-      const uint64_t hb = __ballot(head);
-      const uint32_t pm = (uint32_t)(hb >> (lane & 48)) & 0xffffu;
-      // lane 0 of every row is a head, so these never carry across rows
-      const uint64_t nz1 = ~hb & 0xfffefffefffefffeull, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
-      const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
-      const float g0 = gf[0][ll], g1 = gf[1][ll];
-      const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
-      // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
-      const float gz[2][2] = {{g0 * az, g1 * az}, {g0 * w[2], g1 * w[2]}};   // [k][f]
-      float vmax = 0.f;   // largest |record value| of the level: the owner's fixed-point scale
-      float v[4][4];
-      RecSlot rs[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {   // sums and slots of the 4 corner rows: 4 counter round trips in flight
-        const int j = c >> 1, kk = c & 1;
-        const float wy = j ? w[1] : ay;
-        const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
-        v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
-        seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
-        vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
-        if (head) rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)k.g.log2T, cx, j ? y0 + kPrimeY : y0,
-                                   kk ? z0 + kPrimeZ : z0);
-        if (!HN_SC_BATCH && head) rec_store(bw, rs[c], v[c]);
-      }
-      if (HN_SC_BATCH && head) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-#if HN_SC_STAGE
-          const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[l & 1][staged ? bl : 0];
-          if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
-            const int q = (int)((bl << ph.log2c) + j);
-            stv[q] = f32x4{v[c][0], v[c][1], v[c][2], v[c][3]};
-            stw[q] = rs[c].word;
-            continue;
-          }
-#endif
-          rec_store(bw, rs[c], v[c]);
-        }
-      }
-#if HN_SC_LANEMAX   // per-lane maxima in LDS (one conflict-free ds_max per level), reduced once per block
-      __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-      vmax = wave_max_f32(vmax);
-      if (lane == 0)
-        __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-      }   // act
-#if HN_SC_STAGE
-      __syncthreads();   // the phase's records are in the pool, its counts final
-      st_flush(l);
-      st_init(l + 1 < 16 ? l + 1 : 0);   // the next phase's bins (other parity), counts unchanged by the flush
-      __syncthreads();   // the pool is free again
-#endif
-    }
   }
   if (k.tv_off[16] > 0) {
     // The TV term's table gradient: one record per x-pair (x0, x0 + 1) of cube
@@ -2334,6 +2378,93 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   });
 }
 
+// HN_B1_ONECOPY 1 (split backward): the coarse and fine units share one code
+// path (the pass is a runtime flag: weights, draw offset, tile index and
+// destination are selects) and the unit's two tiles run as a loop, so the
+// kernel holds ONE copy of b1_tile instead of four (two unrolled tiles x two
+// unit templates): 87 KB of code -> ~25 KB, under the 64 KB instruction cache
+// two CUs share (wave 0 ran the coarse copies, waves 1-3 the fine ones, at
+// the same time).
+#ifndef HN_B1_ONECOPY
+#define HN_B1_ONECOPY 1
+#endif
+HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float* X, DW& dw, WRing& wr,
+                          PhaseClock& pc, UnitPre* pre) {
+  pc.start();
+  const int lane = lane_id();
+  const int p = lane & 31, h = lane >> 5;
+  Ray r;
+  if (pre != nullptr) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) r.vd[a] = pre->vd[a];
+  } else {
+    load_ray(k.rays, ray, r);
+  }
+  const int tile0 = 2 * part;
+  const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
+  float4 dr[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(drs + 128 * t);
+  float sh8[8], shx8[8];
+  ray_sh(r, h, sh8, shx8);
+  {
+    const SP<2> sp = splitn<2>([&](int j) { return shx8[j]; });
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const u32x4 w = __builtin_bit_cast(u32x4, sp.p[q]);
+      put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h, w[0], w[1]);
+      put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h + 1, w[2], w[3]);
+    }
+  }
+  const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
+  C0Sh c0sh;
+#if HN_C0SH_LDS
+  {
+    float* cl = X + kC0shF;
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) {
+      const f32x16 v = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+      if (p == 0)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(cl + 32 * ob + row_of(4 * g, h)) =
+              f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+    }
+    lds_fence_wave();
+    c0sh.lds = cl;
+  }
+#else
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob)
+    c0sh.v[ob] = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+#endif
+  const int ctile = (fine ? kSc / 32 : 0) + tile0;
+  f32x16 feat, featn;
+  if (pre != nullptr)
+    feat = pre->feat;
+  else
+    load_feat(k.feat, ray, ctile, lane, feat);
+  load_feat(k.feat, ray, ctile + 1, lane, featn);
+  // this unit's feature-grad tiles (the saved-feature tile order of both passes)
+  f32x4* dst0 = fine ? reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + tile0) * 1024)
+                     : reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)tile0 * 1024);
+  HN_LAP(pc, unit);
+#pragma clang loop unroll(disable)
+  for (int t = 0; t < 2; ++t) {
+    const float4 drt = t ? dr[1] : dr[0];
+    const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, drt, dw, [&]() {
+      if (t == 1 && pre != nullptr && pre->next >= 0)   // the next unit's first inputs, during tile 1
+        unit_pre_load(k, pre->next, (fine ? kSc / 32 : 0) + tile0, lane, *pre);
+    });
+    HN_LAP(pc, mlp);
+    f32x4* dst = dst0 + 256 * t;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dst[64 * c + lane] = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
+    feat = featn;
+    HN_LAP(pc, scat);
+  }
+}
+
 // Composite backward pre-pass (raw2outputs backward, run_nerf_helpers.py:577-628
 // via the :541 / :558 chain): one wave per (ray, pass) at full occupancy
 // writes d raw of every sample, so the MLP units only load one float4 per
@@ -2511,6 +2642,23 @@ void render_bwd_kernel(B1K k) {
 #if HN_PROFILE
     if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
 #endif
+  } else if (SPLIT && HN_B1_ONECOPY) {
+    // split: wave 0 the block's coarse units (slab slot 0), waves 1-3 part
+    // wave - 1 of every ray's fine units (slots 1-3) -- a static split, so each
+    // dW slab, and with the fixed-order slab reduce the MLP gradients, are
+    // bitwise reproducible
+    UnitPre pre;
+    UnitPre* prep = HN_B1_PREFETCH ? &pre : nullptr;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform (SGPR) pass and part
+    const bool fine = wv != 0;
+    const int part = fine ? wv - 1 : 0;
+    wring_prime(wr, fine ? k.Pf : k.Pc, lane);
+    if (prep && n_rays > 0) unit_pre_load(k, block_ray(0), (fine ? kSc / 32 : 0) + 2 * part, lane, pre);
+    for (int i = 0; i < n_rays; ++i) {
+      pre.next = i + 1 < n_rays ? block_ray(i + 1) : -1;
+      b1_unit_split(k, block_ray(i), part, fine, X, dw, wr, pc, prep);
+    }
+    dw_flush<true>(dw, k.slab + ((size_t)blockIdx.x * kSlabSlots + wv) * W_END, lane);
   } else {
     UnitPre pre;
     UnitPre* prep = SPLIT && HN_B1_PREFETCH ? &pre : nullptr;
