@@ -16,8 +16,8 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 9                 # HN_ABI_VERSION
-RENDER_FEAT_PER_RAY = 8192      # HN_RENDER_FEAT_PER_RAY
+ABI_VERSION = 10                # HN_ABI_VERSION
+RENDER_FEAT_PER_RAY = 9728      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
 

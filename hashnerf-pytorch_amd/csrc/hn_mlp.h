@@ -163,7 +163,15 @@ struct MlpAct {
   f32x16 s1;
   f32x16 c0[2];
   f32x16 c1[2];
+  uint32_t m[3];   // ReLU masks of h0, c0, c1 (bit 16 ob + r: value > 0), formed as each is ReLU'd
 };
+// mask bits of one ReLU'd D-layout block: its values are +0 or positive, so a
+// bit is (bits + 0x7fffffff) >> 31 (integer ops only: the compare forms, which
+// min(bits, 1) also becomes, hold lane masks in SGPR pairs and spilled the forward)
+HN_DEV void relu_mask_or(const f32x16& v, uint32_t& m, int ob) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) m |= ((__float_as_uint(v[r]) + 0x7fffffffu) >> 31) << (16 * ob + r);
+}
 
 HN_DEV void relu16(f32x16& v) {
 #pragma unroll
@@ -177,11 +185,13 @@ HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 
 // Forward of one tile.  Returns activations (post-ReLU) and c2 (raw rgb).
 HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const float sh8[8],
                          MlpAct& a, f32x16& c2, int lane) {
+  a.m[0] = a.m[1] = a.m[2] = 0u;
   // sigma_net.0: 32 -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
     a.h0[ob] = gemm<R_F0>(P, ob, zero16(), lane, [&](int s) { return feat[s]; });
     relu16(a.h0[ob]);
+    relu_mask_or(a.h0[ob], a.m[0], ob);
   }
   // sigma_net.1: 64 -> 16 (sigma, geo15), no activation
   a.s1 = gemm<R_F1>(P, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
@@ -191,6 +201,7 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
     f32x16 acc = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
     acc = gemm<R_F2G>(P, ob, acc, lane, [&](int s) { return a.s1[s]; });
     relu16(acc);
+    relu_mask_or(acc, a.m[1], ob);
     a.c0[ob] = acc;
   }
   // color_net.1: 64 -> 64, ReLU
@@ -198,6 +209,7 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   for (int ob = 0; ob < 2; ++ob) {
     a.c1[ob] = gemm<R_F3>(P, ob, zero16(), lane, [&](int s) { return a.c0[s >> 4][s & 15]; });
     relu16(a.c1[ob]);
+    relu_mask_or(a.c1[ob], a.m[2], ob);
   }
   // color_net.2: 64 -> 3, no activation
   c2 = gemm<R_F4>(P, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });

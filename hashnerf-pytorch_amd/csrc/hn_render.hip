@@ -109,11 +109,35 @@ HN_DEV void ray_point(const Ray& r, float z, float pt[3]) {
 // Saved features: tile t of a ray (t = 0,1 coarse, 2..7 fine) is 1024 floats,
 // stored as 4 chunks of [64 lanes][float4] so that both the forward's store
 // and the backward's load are fully coalesced dwordx4 accesses.
+// After the 8 feature tiles: the tiles' ReLU masks of the two networks (tile
+// t: 3 words [h0 | c0 | c1] x 64 lanes, bit 16 ob + r = D register r of
+// output block ob of the lane), written by the forward when HN_B1_SMASK.
 constexpr int kTilesPerRay = (kSc + kSf) / 32;
-static_assert(kTilesPerRay * 1024 == HN_RENDER_FEAT_PER_RAY, "feature cache layout");
+constexpr int kMaskWordsPerTile = 3 * 64;
+static_assert(kTilesPerRay * (1024 + kMaskWordsPerTile) == HN_RENDER_FEAT_PER_RAY, "feature cache layout");
 
+// HN_B1_SMASK 1: the forward stores its ReLU masks and the backward's forward
+// recompute uses them with 2-part products (HN_SPLIT_R 2): the recomputed
+// activations then differ from the forward's by ~2^-17 relative (the dW
+// operands' own precision), but every ReLU decision is the forward's.
+#ifndef HN_B1_SMASK
+#define HN_B1_SMASK 0
+#endif
+
+HN_DEV void store_masks(float* __restrict__ base, int64_t ray, int tile, int lane, const uint32_t (&m)[3]) {
+  uint32_t* t = reinterpret_cast<uint32_t*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024) +
+                tile * kMaskWordsPerTile;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) __builtin_nontemporal_store(m[j], t + 64 * j + lane);
+}
+HN_DEV void load_masks(const float* __restrict__ base, int64_t ray, int tile, int lane, uint32_t (&m)[3]) {
+  const uint32_t* t = reinterpret_cast<const uint32_t*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY +
+                                                        kTilesPerRay * 1024) + tile * kMaskWordsPerTile;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) m[j] = __builtin_nontemporal_load(t + 64 * j + lane);
+}
 HN_DEV void store_feat(float* __restrict__ base, int64_t ray, int tile, int lane, const f32x16& feat) {
-  f32x4* t = reinterpret_cast<f32x4*>(base + ((size_t)ray * kTilesPerRay + tile) * 1024);
+  f32x4* t = reinterpret_cast<f32x4*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + (size_t)tile * 1024);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const f32x4 v = {feat[4 * c], feat[4 * c + 1], feat[4 * c + 2], feat[4 * c + 3]};
@@ -122,7 +146,7 @@ HN_DEV void store_feat(float* __restrict__ base, int64_t ray, int tile, int lane
 }
 
 HN_DEV void load_feat(const float* __restrict__ base, int64_t ray, int tile, int lane, f32x16& feat) {
-  const f32x4* t = reinterpret_cast<const f32x4*>(base + ((size_t)ray * kTilesPerRay + tile) * 1024);
+  const f32x4* t = reinterpret_cast<const f32x4*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + (size_t)tile * 1024);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const f32x4 v = __builtin_nontemporal_load(t + 64 * c + lane);
@@ -281,6 +305,9 @@ void render_fwd_kernel(RenderK k) {
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
+    if (HN_B1_SMASK && k.feat) {
+      store_masks(k.feat, ray, tau, lane, a.m);
+    }
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -329,6 +356,9 @@ void render_fwd_kernel(RenderK k) {
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile(P, feat, sh8, a, c2, lane);
+    if (HN_B1_SMASK && k.feat) {
+      store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);
+    }
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -543,7 +573,7 @@ constexpr int kNSegs = sizeof(kSegs) / sizeof(kSegs[0]);
 // for every part count, so the recompute streams only groups q < HN_SPLIT_R of
 // each chunk).  3 = the forward's own products (bit-identical activations).
 #ifndef HN_SPLIT_R
-#define HN_SPLIT_R 3
+#define HN_SPLIT_R (HN_B1_SMASK ? 2 : 3)
 #endif
 constexpr int seg_ns(const GemmSeg& g) {   // parts this stream uses per chunk (0: f32)
   return g.r < R_B4 && reg_ns(g.r) > HN_SPLIT_R ? HN_SPLIT_R : reg_ns(g.r);
@@ -896,7 +926,7 @@ __device__ unsigned long long g_tile[9];
 #endif
 template <typename AfterFwd>
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
-                      const C0Sh& c0sh, float4 dr, DW& dw, AfterFwd&& after_fwd) {
+                      const C0Sh& c0sh, float4 dr, DW& dw, const uint32_t (&sm)[3], AfterFwd&& after_fwd) {
 #if HN_B1_LANE_OPAQUE
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
 #else
@@ -904,7 +934,14 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
 #endif
   const int h = lane >> 5;
   char* Xb = reinterpret_cast<char*>(X);
+#if HN_B1_SMASK   // the forward's ReLU masks (the recompute's own bits go to a dead word)
+  uint32_t mh0 = sm[0], mc0 = sm[1], mc1 = sm[2], mdead = 0;
+#define HN_RELU(v, m, ob) relu_bits(v, mdead, ob)
+#else
+  (void)sm;
   uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
+#define HN_RELU(v, m, ob) relu_bits(v, m, ob)
+#endif
 #if HN_TILE_PROF
   uint64_t t_ts = 0;
   HN_TSTAMP(-1);
@@ -913,22 +950,22 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   // operand's parts as a dW operand image ----
   f32x16 h0[2] = {zero16(), zero16()};
   gemm2<R_F0, kBF>(wr, P, h0, lane, [&](int s) { return feat[s]; }, Xb);
-  relu_bits(h0[0], mh0, 0);
-  relu_bits(h0[1], mh0, 1);
+  HN_RELU(h0[0], mh0, 0);
+  HN_RELU(h0[1], mh0, 1);
   HN_TSTAMP(0);
   const f32x16 s1 = gemm_w<seg_of(R_F1), kBH0>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; }, Xb);
   f32x16 c0[2];
   c0sh_seed(c0sh, c0, h);
   // s1 rows 0..15 = [sigma | geo15] -> features 16..31 of [sh16 | sigma | geo15]
   gemm2<R_F2G, kBC0in, 4>(wr, P, c0, lane, [&](int s) { return s1[s]; }, Xb);
-  relu_bits(c0[0], mc0, 0);
-  relu_bits(c0[1], mc0, 1);
+  HN_RELU(c0[0], mc0, 0);
+  HN_RELU(c0[1], mc0, 1);
   HN_TSTAMP(1);
   {
     f32x16 c1[2] = {zero16(), zero16()};
     gemm2<R_F3, kBC0>(wr, P, c1, lane, [&](int s) { return c0[s >> 4][s & 15]; }, Xb);
-    relu_bits(c1[0], mc1, 0);
-    relu_bits(c1[1], mc1, 1);
+    HN_RELU(c1[0], mc1, 0);
+    HN_RELU(c1[1], mc1, 1);
     put_tile(Xb, kBC1, c1[0], lane);
     put_tile(Xb, kBC1 + 1, c1[1], lane);
   }
@@ -998,6 +1035,10 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   });
   tile_lds_order();                             // image reads done before any later writes
   HN_TSTAMP(7);
+#if HN_B1_SMASK
+  (void)mdead;
+#endif
+#undef HN_RELU
   return dfeat;
 }
 
@@ -2328,7 +2369,9 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 #pragma unroll
     for (int r = 0; r < 16; ++r) dfeat[r] *= dr[t].x;
 #else
-    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw, [&]() {
+    uint32_t sm[3] = {0u, 0u, 0u};
+    if (HN_B1_SMASK) load_masks(k.feat, ray, ctile + t, lane, sm);
+    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw, sm, [&]() {
       if (t == 1 && pre != nullptr && pre->next >= 0)   // the next unit's first inputs, during tile 1
         unit_pre_load(k, pre->next, ctile, lane, *pre);
     });
@@ -2452,7 +2495,9 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
 #pragma clang loop unroll(disable)
   for (int t = 0; t < 2; ++t) {
     const float4 drt = t ? dr[1] : dr[0];
-    const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, drt, dw, [&]() {
+    uint32_t sm[3] = {0u, 0u, 0u};
+    if (HN_B1_SMASK) load_masks(k.feat, ray, ctile + t, lane, sm);
+    const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, drt, dw, sm, [&]() {
       if (t == 1 && pre != nullptr && pre->next >= 0)   // the next unit's first inputs, during tile 1
         unit_pre_load(k, pre->next, (fine ? kSc / 32 : 0) + tile0, lane, *pre);
     });

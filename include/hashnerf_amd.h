@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 9
+#define HN_ABI_VERSION 10
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -149,7 +149,8 @@ typedef struct hn_render_cfg {
   int32_t reserved;
 } hn_render_cfg;
 
-#define HN_RENDER_FEAT_PER_RAY 8192   /* (64 + 192) points x 16 levels x 2 features */
+#define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the
+                                         MLPs' ReLU masks of those points (ABI 10) */
 
 typedef struct hn_render_fwd_args {
   int64_t n_rays;
@@ -173,8 +174,8 @@ typedef struct hn_render_fwd_args {
   float* raw_f;             /* [B][192][4] */
   uint8_t* fine_src;        /* [B][192]: coarse index of each fine sample, 255 = importance */
   float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
-                               evaluated points (MFMA-tile order, opaque); NULL = not kept
-                               (inference); required by hn_render_bwd */
+                               evaluated points and their ReLU masks (MFMA-tile order,
+                               opaque); NULL = not kept (inference); required by hn_render_bwd */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
