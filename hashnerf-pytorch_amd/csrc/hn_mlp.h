@@ -183,6 +183,10 @@ HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 
 }
 
 // Forward of one tile.  Returns activations (post-ReLU) and c2 (raw rgb).
+// MASKS: also form a.m (pinned right after each ReLU by an empty asm, so the
+// compiler cannot sink the bit ops to the masks' late use and keep every
+// activation live until then -- that spilled the render forward 39 -> 158).
+template <bool MASKS = false>
 HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const float sh8[8],
                          MlpAct& a, f32x16& c2, int lane) {
   a.m[0] = a.m[1] = a.m[2] = 0u;
@@ -191,8 +195,9 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   for (int ob = 0; ob < 2; ++ob) {
     a.h0[ob] = gemm<R_F0>(P, ob, zero16(), lane, [&](int s) { return feat[s]; });
     relu16(a.h0[ob]);
-    relu_mask_or(a.h0[ob], a.m[0], ob);
+    if constexpr (MASKS) relu_mask_or(a.h0[ob], a.m[0], ob);
   }
+  if constexpr (MASKS) asm volatile("" : "+v"(a.m[0]));
   // sigma_net.1: 64 -> 16 (sigma, geo15), no activation
   a.s1 = gemm<R_F1>(P, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
   // color_net.0: [sh16 | geo15] -> 64, ReLU
@@ -201,16 +206,18 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
     f32x16 acc = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
     acc = gemm<R_F2G>(P, ob, acc, lane, [&](int s) { return a.s1[s]; });
     relu16(acc);
-    relu_mask_or(acc, a.m[1], ob);
+    if constexpr (MASKS) relu_mask_or(acc, a.m[1], ob);
     a.c0[ob] = acc;
   }
+  if constexpr (MASKS) asm volatile("" : "+v"(a.m[1]));
   // color_net.1: 64 -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
     a.c1[ob] = gemm<R_F3>(P, ob, zero16(), lane, [&](int s) { return a.c0[s >> 4][s & 15]; });
     relu16(a.c1[ob]);
-    relu_mask_or(a.c1[ob], a.m[2], ob);
+    if constexpr (MASKS) relu_mask_or(a.c1[ob], a.m[2], ob);
   }
+  if constexpr (MASKS) asm volatile("" : "+v"(a.m[2]));
   // color_net.2: 64 -> 3, no activation
   c2 = gemm<R_F4>(P, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });
 }

@@ -304,10 +304,8 @@ void render_fwd_kernel(RenderK k) {
     HN_FT(0);
     MlpAct a;
     f32x16 c2;
-    mlp_fwd_tile(P, feat, sh8, a, c2, lane);
-    if (HN_B1_SMASK && k.feat) {
-      store_masks(k.feat, ray, tau, lane, a.m);
-    }
+    mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
+    if (k.feat) store_masks(k.feat, ray, tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -355,10 +353,8 @@ void render_fwd_kernel(RenderK k) {
     HN_FT(3);
     MlpAct a;
     f32x16 c2;
-    mlp_fwd_tile(P, feat, sh8, a, c2, lane);
-    if (HN_B1_SMASK && k.feat) {
-      store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);
-    }
+    mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
+    if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -1707,7 +1703,7 @@ struct ScK {
 #define HN_SC_PERM 0
 #endif
 #ifndef HN_SC_ROLL   // 1: levels in a rolled loop of level pairs (one copy of the level code)
-#define HN_SC_ROLL 0
+#define HN_SC_ROLL 1
 #endif
 constexpr int kScWaves = 16;
 #ifndef HN_SC_LGROUP   // levels per scatter pass (16: all levels per unit at once; 4: level-group major,
