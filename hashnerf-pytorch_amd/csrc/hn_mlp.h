@@ -165,12 +165,23 @@ struct MlpAct {
   f32x16 c1[2];
   uint32_t m[3];   // ReLU masks of h0, c0, c1 (bit 16 ob + r: value > 0), formed as each is ReLU'd
 };
+#ifndef HN_MASK_ASM
+#define HN_MASK_ASM 0
+#endif
 // mask bits of one ReLU'd D-layout block: its values are +0 or positive, so a
 // bit is (bits + 0x7fffffff) >> 31 (integer ops only: the compare forms, which
 // min(bits, 1) also becomes, hold lane masks in SGPR pairs and spilled the forward)
 HN_DEV void relu_mask_or(const f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) m |= ((__float_as_uint(v[r]) + 0x7fffffffu) >> 31) << (16 * ob + r);
+  for (int r = 0; r < 16; ++r) {
+#if HN_MASK_ASM   // v_min_u32 (the compiler turns min(bits, 1) into a compare + select)
+    uint32_t b;
+    asm("v_min_u32 %0, %1, 1" : "=v"(b) : "v"(__float_as_uint(v[r])));
+    m |= b << (16 * ob + r);
+#else
+    m |= ((__float_as_uint(v[r]) + 0x7fffffffu) >> 31) << (16 * ob + r);
+#endif
+  }
 }
 
 HN_DEV void relu16(f32x16& v) {

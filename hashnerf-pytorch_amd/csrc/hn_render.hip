@@ -121,7 +121,7 @@ static_assert(kTilesPerRay * (1024 + kMaskWordsPerTile) == HN_RENDER_FEAT_PER_RA
 // activations then differ from the forward's by ~2^-17 relative (the dW
 // operands' own precision), but every ReLU decision is the forward's.
 #ifndef HN_B1_SMASK
-#define HN_B1_SMASK 0
+#define HN_B1_SMASK 1
 #endif
 
 HN_DEV void store_masks(float* __restrict__ base, int64_t ray, int tile, int lane, const uint32_t (&m)[3]) {

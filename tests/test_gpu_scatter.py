@@ -148,7 +148,10 @@ def test_forward_state_deterministic(hn):
     *_, s1, g1 = _state(hn, 1024, 19, 17, "binned", box=box)
     *_, s2, g2 = _state(hn, 1024, 19, 17, "binned", box=box)
     for name in ("z_f", "raw_c", "raw_f", "feat", "fine_src"):
-        assert torch.equal(getattr(s1, name), getattr(s2, name)), name
+        a, b = getattr(s1, name), getattr(s2, name)
+        if name == "feat":   # compared bitwise: its ReLU mask words (ABI 10) read as floats include NaN patterns
+            a, b = a.view(torch.int32), b.view(torch.int32)
+        assert torch.equal(a, b), name
     for k in g1:
         assert torch.equal(g1[k], g2[k]), k
 
