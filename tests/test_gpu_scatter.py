@@ -86,8 +86,8 @@ def test_binned_matches_atomic(hn, T, B):
     assert _rel(tb, ta) <= 1e-6, _rel(tb, ta)
     # same MLP backward, summed over the tiles in another order (split
     # schedule: wave 0 coarse, waves 1-3 fine) -- fp32 summation-order level
-    for x, y in zip(wb, wa):
-        assert _rel(x, y) <= 1e-4, _rel(x, y)
+    rels = [_rel(x, y) for x, y in zip(wb, wa)]
+    assert max(rels) <= 1e-4, rels
 
 
 def test_binned_bitwise_reproducible_and_overwrite(hn):
@@ -132,8 +132,8 @@ def test_binned_clumped_box(hn):
     ta, wa = _bwd(HF, emb, ws, st_a, grads_a)
     assert torch.count_nonzero(tb) > 0
     assert _rel(tb, ta) <= 1e-6, _rel(tb, ta)
-    for x, y in zip(wb, wa):
-        assert _rel(x, y) <= 1e-4, _rel(x, y)
+    rels = [_rel(x, y) for x, y in zip(wb, wa)]
+    assert max(rels) <= 1e-4, rels
     # the same forward state with every region capped at 64 records (a
     # smaller layout inside the same workspace): most records spill
     st_b.cfg.bin_cap = 64
