@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--ray-order", type=int, default=1, choices=(0, 1),
                     help="batch order from the sampler: 1 Morton order of the pixels, 0 draw order")
+    ap.add_argument("--dense-table-step", action="store_true",
+                    help="A/B: the fused table step over every row (no live-pair mask)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -239,6 +241,7 @@ def main():
     if "bbox" in cfg:
         data.bounding_box = tuple(torch.tensor(v) for v in cfg["bbox"])
     tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0, ray_order=args.ray_order)
+    tr.skip_dead_rows = not args.dense_table_step
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1
@@ -274,6 +277,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     bwd_ms = HF.TIMER.mean_ms("render_bwd")
+    # diagnostic, after the timed region: the host's time to enqueue one step
+    # (Python + ctypes; the device runs concurrently) -- at or above
+    # ms_per_step the host, not the GPU, would set the step rate
+    host = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        tr.step()
+        host.append(time.perf_counter() - h0)
+    torch.cuda.synchronize()
+    host_ms = 1e3 * sorted(host)[len(host) // 2]
     B = cfg["N_rand"]
     value = world * B * args.steps / dt
     if rank == 0:
@@ -316,6 +330,7 @@ def main():
                          "path": {"bytes_per_ray": PATH_BYTES_PER_RAY, "achieved": round(path_gbs, 1),
                                   "frac": round(path_gbs / HBM_PEAK_GBS, 4),
                                   "meaning": "gather + scatter-add + ray I/O per ray x rays/s (whole step)"}},
+            "host_enqueue_ms": round(host_ms, 3),
             "kernels": {"render_fwd_ms": round(fwd_ms, 4), "render_fwd_GBs": round(fwd_gbs, 1),
                         "render_bwd_ms": round(bwd_ms, 4),
                         "path_GBs": round(path_gbs, 1), "path_frac": round(path_gbs / HBM_PEAK_GBS, 4)},

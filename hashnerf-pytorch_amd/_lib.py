@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 10                # HN_ABI_VERSION
+ABI_VERSION = 11                # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 9728      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -72,7 +72,8 @@ class HnRenderBwdArgs(C.Structure):
                 ("d_table_mode", C.c_int32), ("g_rgb", _P), ("g_depth", _P), ("g_acc", _P), ("g_sparsity", _P),
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
-                ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P)]
+                ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
+                ("table_live", _P), ("table_live_levels", C.c_int32), ("reserved", C.c_int32)]
 
 
 class HnTvArgs(C.Structure):
@@ -162,7 +163,8 @@ def check(status: int, what: str):
 
 FAULT_BITS = {1: "ring slot wait", 2: "ring drain (tiles left unscattered)", 4: "coarse-grad flag wait",
               8: "dW buffer wait", 16: "binned-scatter overflow records exhausted",
-              32: "non-finite (NaN / Inf) feature gradient or sample point in the binned scatter"}
+              32: "non-finite (NaN / Inf) feature gradient or sample point in the binned scatter",
+              64: "gradient on a table row pair the live mask marks dead (fused table step)"}
 
 
 def check_device_faults(clear: bool = True):

@@ -77,6 +77,9 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 // acc += A(region R, block ob) . B where bval(s) is the B operand of f32 k-step s.
 // The next A fragments are loaded while the current ones' MFMAs run; the
 // scheduling barrier stops hipcc from hoisting all loads (register blowup).
+#ifndef HN_GEMM_TAILNOP
+#define HN_GEMM_TAILNOP 0
+#endif
 #ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk
 #define HN_GEMM_PF 1
 #endif
@@ -143,6 +146,9 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
 #endif
       __builtin_amdgcn_sched_barrier(0);
     }
+#if HN_GEMM_TAILNOP   // diagnostic: 16 extra wait states between a GEMM's last MFMA and any reader
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
     return acc;
   } else {
     f32x4 an = ld(0);

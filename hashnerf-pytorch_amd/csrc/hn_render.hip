@@ -123,6 +123,9 @@ static_assert(kTilesPerRay * (1024 + kMaskWordsPerTile) == HN_RENDER_FEAT_PER_RA
 #ifndef HN_B1_SMASK
 #define HN_B1_SMASK 1
 #endif
+#ifndef HN_FWD_DBG
+#define HN_FWD_DBG 0
+#endif
 
 HN_DEV void store_masks(float* __restrict__ base, int64_t ray, int tile, int lane, const uint32_t (&m)[3]) {
   uint32_t* t = reinterpret_cast<uint32_t*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024) +
@@ -305,7 +308,17 @@ void render_fwd_kernel(RenderK k) {
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
+#if HN_FWD_DBG   // diagnostic: coarse tile 0's sh8 and s1 registers in place of the mask words
+    if (k.feat && tau == 0) {
+      uint32_t* dbg = reinterpret_cast<uint32_t*>(k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dbg[64 * j + lane] = __float_as_uint(sh8[j]);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dbg[64 * (8 + j) + lane] = __float_as_uint(a.s1[j]);
+    }
+#else
     if (k.feat) store_masks(k.feat, ray, tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
+#endif
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -354,7 +367,9 @@ void render_fwd_kernel(RenderK k) {
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
+#if !HN_FWD_DBG
     if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
+#endif
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -1519,7 +1534,7 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // autograd would propagate it into embeddings[l].grad, hash_encoding.py:106),
 // so the gradient of that launch is flagged invalid instead of silently
 // dropping the contribution.
-enum : int { kFaultBins = 16, kFaultNonFinite = 32 };
+enum : int { kFaultBins = 16, kFaultNonFinite = 32, kFaultDeadRow = 64 };
 
 // Record r in memory.  HN_REC_AOS 0 (default): the values [nrec] f32x4 then
 // the words [nrec] u32.  HN_REC_AOS 1: groups of 4 records = 4 value quads
@@ -2853,6 +2868,8 @@ struct BinR {
   int32_t overwrite;
   int32_t fused;           // 1: apply `step` to the table (p, m, v) with the bin's gradient
   hn_radam_tensor step;
+  const uint32_t* live;    // fused step: live row pairs of levels < live_levels (hn_render_bwd_args.table_live)
+  int32_t live_levels;
 };
 constexpr int kBinThreads = 1024;
 constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2^13 floats / 4 / 1024)
@@ -2999,11 +3016,18 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
   const int nd4 = (2 << k.shift) / 4;             // float4s of the slice (<= 4 per thread)
   float4 sp[kSliceF4], sm[kSliceF4], sv[kSliceF4];
+  // fused step on a coarse level: the row pairs no gradient can reach (their
+  // moments are zero, so the dense update leaves p, m, v bitwise unchanged)
+  // are neither loaded nor stored (table_live; T=19: levels 0-6)
+  const uint32_t* lw = nullptr;
+  if (k.fused && k.live && k.shift <= k.log2T && (int)(((uint32_t)b << k.shift) >> k.log2T) < k.live_levels)
+    lw = k.live + (((size_t)b << k.shift) >> 6);
+  auto live_at = [&](int i) { return lw == nullptr || ((lw[i >> 5] >> (i & 31)) & 1u) != 0u; };
   auto load_state = [&]() {
 #pragma unroll
     for (int j = 0; j < kSliceF4; ++j) {
       const int i = threadIdx.x + j * kBinThreads;
-      if (i < nd4) {
+      if (i < nd4 && live_at(i)) {
         sp[j] = reinterpret_cast<const float4*>(k.step.p + e0)[i];
         sm[j] = reinterpret_cast<const float4*>(k.step.m + e0)[i];
         sv[j] = reinterpret_cast<const float4*>(k.step.v + e0)[i];
@@ -3155,7 +3179,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       }
       dst[i] = a;
     }
-    if (k.fused) {   // RAdam on these 4 table elements (radam_kernel's update, same op forms)
+    if (k.fused && !live_at(i)) {   // a dead pair: its gradient is a structural zero
+      if (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f)
+        __hip_atomic_fetch_or(&g_hn_fault, kFaultDeadRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (k.fused) {   // RAdam on these 4 table elements (radam_kernel's update, same op forms)
       if (HN_BR_PF == 0) {
         sp[j] = reinterpret_cast<const float4*>(k.step.p + e0)[i];
         sm[j] = reinterpret_cast<const float4*>(k.step.m + e0)[i];
@@ -3403,6 +3430,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     const hn_radam_tensor& ts = *a->table_step;
     if (mode != kModeSplit || ts.n != ((int64_t)16 << cfg->grid.log2_hashmap_size) * 2) return HN_E_SHAPE;
     if (!ts.p || !ts.m || !ts.v) return HN_E_NULL;
+    if (a->table_live && (a->table_live_levels < 0 || a->table_live_levels > cfg->grid.n_levels || T < 6))
+      return HN_E_SHAPE;
   }
   // TV term: records of the binned scatter, or hn_tv_bwd into d_table (atomic schedule)
   TvK tvk;
@@ -3489,6 +3518,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     r.overwrite = (a->d_table_mode & 1) != 0;
     r.fused = a->table_step != nullptr;
     if (r.fused) r.step = *a->table_step;
+    r.live = r.fused ? a->table_live : nullptr;
+    r.live_levels = r.live ? a->table_live_levels : 0;
     hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
     if ((st = hip_status(hipGetLastError()))) return st;
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),

@@ -259,7 +259,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
 
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
-               overwrite_mlp: bool = False, tv=None):
+               overwrite_mlp: bool = False, tv=None, table_live=None):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -271,7 +271,10 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     tv = (min_vertex [L, 3] device int32, cubes, g_tv [L]) from tv_fwd and the
     loss backward: the TV term's table gradient (loss.py:11-43) joins this
     backward -- as records of the binned owner pass (so table_step stays
-    fused), or added to d_table -- instead of a separate tv_bwd."""
+    fused), or added to d_table -- instead of a separate tv_bwd.
+    table_live = (n_levels, int32 bitmap) from train.live_pair_mask, with
+    table_step: the fused step skips the row pairs no gradient can reach
+    (bitwise the same update, fewer optimizer-state bytes)."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -307,6 +310,15 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
                   "mode", "has_wd"):
             setattr(step, k, c[k])
         a.table_step = C.pointer(step)
+        if table_live is not None:
+            n_lv, words = table_live
+            if not words.is_cuda or words.dtype != torch.int32 or not words.is_contiguous() or \
+                    words.numel() < (n_lv << st.cfg.grid.log2_hashmap_size) // 64:
+                raise ValueError("hashnerf_amd.render_bwd: table_live must be a contiguous device int32 "
+                                 "bitmap of n_levels << (T - 6) words")
+            keep.append(words)
+            a.table_live = words.data_ptr()
+            a.table_live_levels = n_lv
     if tv is not None:
         mv, cubes, g_tv = tv
         tva = _tv_args(st.table, mv, cubes, st.cfg.grid.log2_hashmap_size)

@@ -73,6 +73,21 @@ def live_rows(resolutions, log2_hashmap_size):
     return n_lv, torch.from_numpy(np.concatenate(idx))
 
 
+def live_pair_mask(resolutions, log2_hashmap_size):
+    """live_rows as the bitmap of hn_render_bwd_args.table_live: bit
+    (R >> 1) & 31 of word R >> 6 is set when row R or R + 1 of the flat
+    [level][row] index is live.  Returns (n_levels, int32 tensor) or None."""
+    lv = live_rows(resolutions, log2_hashmap_size)
+    if lv is None or log2_hashmap_size < 6:
+        return None
+    n_lv, rows = lv
+    pairs = rows.numpy().astype(np.uint64) >> np.uint64(1)
+    words = np.zeros(n_lv << (log2_hashmap_size - 6), dtype=np.uint32)
+    np.bitwise_or.at(words, (pairs >> np.uint64(5)).astype(np.int64),
+                     (np.uint32(1) << (pairs & np.uint64(31)).astype(np.uint32)))
+    return n_lv, torch.from_numpy(words.view(np.int32))
+
+
 def allreduce_grads(table, mlp_params, group=None, live=None):
     """SUM all-reduce of the hash-table gradient and of the flattened
     NeRFSmall gradients, issued asynchronously back to back so RCCL can run
@@ -382,6 +397,9 @@ class Trainer:
         # explicit mode, one GPU: fuse the table's RAdam step into the binned
         # backward's owner pass when the step has no TV term
         self.fuse_table_step = True
+        # ... and skip the coarse levels' unreachable row pairs there
+        # (live_pair_mask: bitwise the same step, fewer optimizer-state bytes)
+        self.skip_dead_rows = True
         # explicit mode, world > 1: reduce-scatter / sharded RAdam / all-gather
         # of the table (ShardedTableStep) instead of all-reduce + full RAdam
         self.dp_sharded = True
@@ -457,6 +475,17 @@ class Trainer:
             lv = live_rows(e.resolutions, e.log2_hashmap_size)
             self._live = None if lv is None else (lv[0], lv[1].to(self.device))
         return self._live
+
+    def _live_mask(self):
+        """train.live_pair_mask on the device (built once), or None when
+        Trainer.skip_dead_rows is off."""
+        if not self.skip_dead_rows:
+            return None
+        if not hasattr(self, "_livem"):
+            e = self.embed_fn
+            lm = live_pair_mask(e.resolutions, e.log2_hashmap_size)
+            self._livem = None if lm is None else (lm[0], lm[1].to(self.device))
+        return self._livem
 
     def allreduce_grads(self):
         if self.world > 1:
@@ -551,7 +580,7 @@ class Trainer:
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True, tv=tvb)
+                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask())
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 10
+#define HN_ABI_VERSION 11
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -76,7 +76,8 @@ const char* hn_status_string(int32_t status);
  * 16 binned-scatter overflow records exhausted (gradient records lost),
  * 32 a NaN / Inf feature gradient or sample point reached the binned scatter
  * (its exact fixed-point sums cannot carry it; the reference's autograd would
- * propagate it into the table gradient).
+ * propagate it into the table gradient), 64 a gradient on a row pair table_live
+ * marks dead (hn_render_bwd_args).
  * Nonzero means the gradients of the launches since the last clear are
  * invalid.  This is the one entry point that synchronises (a blocking copy
  * from the device); call it at points where the host syncs anyway.
@@ -213,6 +214,19 @@ typedef struct hn_render_bwd_args {
    * NULL = no TV term. */
   const struct hn_tv_args* tv;
   const float* g_tv;
+  /* Optional with table_step (ABI 11): the live row pairs of the table's leading
+   * table_live_levels levels, a device bitmap over the flat [level][row] index:
+   * bit (R >> 1) & 31 of word R >> 6 covers rows R and R + 1.  A clear bit
+   * promises that neither row can ever receive a gradient (render or TV: level l's
+   * corners lie in [0, res_l + 1]^3 once the point is clamped to the box,
+   * hash_encoding.py:66-76, so the other rows of a level with (res_l + 2)^3 < 2^T
+   * are structural zeros) and that their moments are zero; the fused step then
+   * neither loads nor stores p / m / v there -- the dense update would leave them
+   * bitwise unchanged.  A nonzero gradient on a clear pair sets fault bit 64.
+   * NULL = every row stepped. */
+  const uint32_t* table_live;
+  int32_t table_live_levels;
+  int32_t reserved;
 } hn_render_bwd_args;
 
 /* ---- L4 hash-table total variation (loss.py:11-43), all levels at once ---

@@ -18,7 +18,8 @@ from scipy import stats
 TOL_DB = 0.1
 out_path, runs = sys.argv[1], [json.load(open(p)) for p in sys.argv[2:]]
 per = [dict(seed=r.get("seed", 0), psnr_hip=r["final"]["psnr_hip"], psnr_ref=r["final"]["psnr_ref"],
-            diff_median=r["final"]["diff"], diff=r["final"].get("diff_mean", r["final"]["diff"]))
+            diff_median=r["final"]["diff"], diff=r["final"].get("diff_mean", r["final"]["diff"]),
+            diff_pmed=r["final"].get("diff_pmed"))
        for r in runs]
 d = np.array([p["diff"] for p in per])
 n = len(d)
@@ -35,5 +36,13 @@ agg = dict(iters=runs[0]["iters"], H=runs[0]["H"], W=runs[0]["W"], N_rand=runs[0
            ci95=[round(mean - half, 4), round(mean + half, 4)],
            parity_shown=bool(n > 1 and abs(mean) + half <= TOL_DB),
            per_seed=per, runs=runs)
+# secondary statistic (reported, not the bar): per run, the median over the
+# tail evaluations of the paired differences (robust to one evaluation's spike)
+dp = np.array([p["diff_pmed"] for p in per if p["diff_pmed"] is not None])
+if len(dp) > 1:
+    se2 = float(dp.std(ddof=1)) / np.sqrt(len(dp))
+    h2 = float(stats.t.ppf(0.975, len(dp) - 1) * se2)
+    agg["secondary_paired_median"] = dict(n=len(dp), mean=round(float(dp.mean()), 4), se=round(se2, 4),
+                                          ci95=[round(float(dp.mean()) - h2, 4), round(float(dp.mean()) + h2, 4)])
 json.dump(agg, open(out_path, "w"), indent=1)
 print(json.dumps({k: v for k, v in agg.items() if k not in ("runs", "per_seed")}))

@@ -163,3 +163,25 @@ def test_live_rows_cover_every_gradient():
     dead[rows] = False
     assert head[~dead].abs().sum() > 0
     assert torch.count_nonzero(head[dead]) == 0
+
+
+def test_live_pair_mask_matches_live_rows():
+    """train.live_pair_mask (hn_render_bwd_args.table_live) sets exactly the
+    pairs (R >> 1) of the rows live_rows returns, at T=19 / finest 512 (levels
+    0-6) and T=22 / finest 1024 (levels 0-8)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn_loader.load()
+    import numpy as np
+    from hashnerf_pytorch_amd.embedding import level_resolutions
+    from hashnerf_pytorch_amd.train import live_pair_mask, live_rows
+    for T, fin, want in ((19, 512, 7), (22, 1024, 9)):
+        _, res = level_resolutions(16, 16, fin)
+        n_lv, rows = live_rows(res, T)
+        n2, words = live_pair_mask(res, T)
+        assert n_lv == n2 == want and words.dtype == torch.int32 and words.numel() == n_lv << (T - 6)
+        bits = np.unpackbits(words.numpy().view(np.uint8), bitorder="little").astype(bool)
+        expect = np.zeros(n_lv << (T - 1), dtype=bool)
+        expect[rows.numpy() >> 1] = True
+        assert np.array_equal(bits, expect)

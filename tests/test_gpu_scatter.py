@@ -214,6 +214,52 @@ def test_fused_table_step_bitwise(hn, mode):
         assert not torch.equal(pf, p0)
 
 
+@pytest.mark.parametrize("mode", [0, 2])
+def test_fused_table_step_live_mask_bitwise(hn, mode):
+    """The fused step with the live-pair bitmap (train.live_pair_mask: the
+    coarse levels' row pairs outside the hashed (res+2)^3 corners are skipped)
+    equals the dense hn_radam_step on the stored gradient, bitwise, when the
+    dead rows' moments are zero (as they always are in training: no gradient
+    ever reaches them).  Then the bitmap with one level's live pairs cleared:
+    the owner sees gradient on a pair marked dead and raises fault bit 64."""
+    from hashnerf_pytorch_amd.train import live_pair_mask, live_rows
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 2048, 19, 9, "binned")
+    n_lv, words = live_pair_mask(emb.resolutions, 19)
+    assert n_lv == 7
+    words = words.to(DEV)
+    _, rows = live_rows(emb.resolutions, 19)
+    live = torch.zeros(16 << 19, dtype=torch.bool, device=DEV)
+    live[rows.to(DEV)] = True
+    live[n_lv << 19:] = True
+    live = live.view(16, 1 << 19, 1)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    p0 = emb.table.detach().clone()
+    m0 = torch.randn(p0.shape, device=DEV, generator=g) * 1e-6 * live
+    v0 = torch.rand(p0.shape, device=DEV, generator=g) * 1e-10 * live
+    c = {"beta1": 0.9, "beta2": 0.99, "one_minus_beta1": 1 - 0.9, "one_minus_beta2": 1 - 0.99, "eps": 1e-15,
+         "neg_wd_lr": 0.0, "neg_step_lr": -0.0421 * 0.01 if mode else 0.0, "mode": mode, "has_wd": 0}
+    pf, mf_, vf = p0.clone(), m0.clone(), v0.clone()
+    HF.render_bwd(st, grads, None, HF.zeros_like_all(ws), table_step=(pf, mf_, vf, c), table_live=(n_lv, words))
+    d_table, _ = _bwd(HF, emb, ws, st, grads)
+    assert torch.count_nonzero(d_table * ~live) == 0, "gradient outside train.live_rows"
+    pr, mr, vr = p0.clone(), m0.clone(), v0.clone()
+    HF.radam_step([(pr, d_table, mr, vr, c)])
+    torch.cuda.synchronize()
+    assert torch.equal(mf_, mr) and torch.equal(vf, vr)
+    assert torch.equal(pf, pr)
+    bad = words.clone()
+    bad[(6 << 19) // 64:(7 << 19) // 64] = 0            # level 6 "dead"
+    keep, HF.CHECK_FAULTS = HF.CHECK_FAULTS, False
+    try:
+        HF.render_bwd(st, grads, None, HF.zeros_like_all(ws), table_step=(p0.clone(), m0.clone(), v0.clone(), c),
+                      table_live=(n_lv, bad))
+    finally:
+        HF.CHECK_FAULTS = keep
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="live mask"):
+        HF.L.check_device_faults()
+
+
 def test_nonfinite_gradient_raises_fault(hn):
     """A NaN upstream gradient on one ray: the reference's autograd carries it
     into embeddings[l].grad (hash_encoding.py:106); the binned owner pass's

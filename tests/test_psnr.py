@@ -168,6 +168,9 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     # the lower-variance statistic the multi-seed aggregate uses: the mean over
     # the tail evaluations of the paired (same-iteration) differences
     stat["diff_mean"] = mean("diff")
+    # secondary, robust to single-evaluation spikes: the median over the tail
+    # evaluations of the paired differences
+    stat["diff_pmed"] = med("diff")
     # scale of the bar: the HIP path alone at other seeds (other images,
     # pixels, jitter and init) -- how far two equally good runs land apart
     seeds = int(os.environ.get("HN_PSNR_SEEDS", "0"))
