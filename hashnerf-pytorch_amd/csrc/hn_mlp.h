@@ -203,9 +203,11 @@ HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 
 // MASKS: also form a.m (pinned right after each ReLU by an empty asm, so the
 // compiler cannot sink the bit ops to the masks' late use and keep every
 // activation live until then -- that spilled the render forward 39 -> 158).
-template <bool MASKS = false>
-HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const float sh8[8],
-                         MlpAct& a, f32x16& c2, int lane) {
+// C0Init(ob): color_net.0's SH half for output block ob (constant along a ray:
+// the fused forward computes it once per ray and seeds every tile with it).
+template <bool MASKS = false, typename C0Init>
+HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0Init&& c0init,
+                            MlpAct& a, f32x16& c2, int lane) {
   a.m[0] = a.m[1] = a.m[2] = 0u;
   // sigma_net.0: 32 -> 64, ReLU
 #pragma unroll
@@ -220,7 +222,7 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   // color_net.0: [sh16 | geo15] -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    f32x16 acc = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+    f32x16 acc = c0init(ob);
     acc = gemm<R_F2G>(P, ob, acc, lane, [&](int s) { return a.s1[s]; });
     relu16(acc);
     if constexpr (MASKS) relu_mask_or(acc, a.m[1], ob);
@@ -237,6 +239,37 @@ HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const 
   if constexpr (MASKS) asm volatile("" : "+v"(a.m[2]));
   // color_net.2: 64 -> 3, no activation
   c2 = gemm<R_F4>(P, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });
+}
+template <bool MASKS = false>
+HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const float sh8[8],
+                         MlpAct& a, f32x16& c2, int lane) {
+  mlp_fwd_tile_c0<MASKS>(P, feat, [&](int ob) { return gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; }); },
+                         a, c2, lane);
+}
+// The SH half of color_net.0 for one ray (every point's column holds the same
+// rows), kept in 64 floats of LDS: lanes 0 and 32 store their rows; a tile
+// then seeds its accumulators with c0sh_lds_load (bitwise the per-tile GEMM).
+HN_DEV void c0sh_lds_store(const float* __restrict__ P, const float sh8[8], float* lds, int lane) {
+  const int p = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    const f32x16 v = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
+    if (p == 0)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(lds + 32 * ob + row_of(4 * g, h)) = f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+  }
+}
+HN_DEV f32x16 c0sh_lds_load(const float* lds, int ob, int lane) {
+  const int h = lane >> 5;
+  f32x16 c;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(lds + 32 * ob + row_of(4 * g, h));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
+  }
+  return c;
 }
 
 // ---------------------------------------------------------------------------

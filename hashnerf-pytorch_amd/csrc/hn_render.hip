@@ -212,7 +212,10 @@ HN_DEV void stage_grid_sizes(const GridArgs& g, float* gsl) {
 
 // LDS per forward wave (floats).
 constexpr int kFZc = 0, kFZsrc = 64, kFZs = 256, kFRaw = 448, kFW = 1216, kFBins = 1280,
-              kFCdf = 1344, kFLds = 1408;
+              kFCdf = 1344, kFC0 = 1408, kFLds = 1472;
+#ifndef HN_FWD_C0SH   // 1: color_net.0's SH half once per ray and net (LDS seed), not per tile
+#define HN_FWD_C0SH 1
+#endif
 
 #ifndef HN_FWD_WAVES_PER_SIMD
 #define HN_FWD_WAVES_PER_SIMD 4
@@ -296,6 +299,11 @@ void render_fwd_kernel(RenderK k) {
   lds_fence_wave();
 
   // ---- coarse network (:540) ----
+  float* c0l = L + kFC0;
+#if HN_FWD_C0SH
+  c0sh_lds_store(opaque_ptr(k.Pc), sh8, c0l, lane);
+  lds_fence_wave();
+#endif
   for (int tau = 0; tau < kSc / 32; ++tau) {
     const float* P = opaque_ptr(k.Pc);
     const int q = 32 * tau + p;
@@ -307,7 +315,11 @@ void render_fwd_kernel(RenderK k) {
     HN_FT(0);
     MlpAct a;
     f32x16 c2;
+#if HN_FWD_C0SH
+    mlp_fwd_tile_c0<HN_B1_SMASK != 0>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
+#else
     mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
+#endif
 #if HN_FWD_DBG   // diagnostic: coarse tile 0's sh8 and s1 registers in place of the mask words
     if (k.feat && tau == 0) {
       uint32_t* dbg = reinterpret_cast<uint32_t*>(k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024);
@@ -355,6 +367,10 @@ void render_fwd_kernel(RenderK k) {
   HN_FT(2);
 
   // ---- fine network (:556) ----
+#if HN_FWD_C0SH
+  c0sh_lds_store(opaque_ptr(k.Pf), sh8, c0l, lane);   // the coarse tiles' reads are done (in-order LDS)
+  lds_fence_wave();
+#endif
   for (int tau = 0; tau < kSf / 32; ++tau) {
     const float* P = opaque_ptr(k.Pf);
     const int q = 32 * tau + p;
@@ -366,7 +382,11 @@ void render_fwd_kernel(RenderK k) {
     HN_FT(3);
     MlpAct a;
     f32x16 c2;
+#if HN_FWD_C0SH
+    mlp_fwd_tile_c0<HN_B1_SMASK != 0>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
+#else
     mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
+#endif
 #if !HN_FWD_DBG
     if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
 #endif
