@@ -261,6 +261,9 @@ def main():
     torch.cuda.synchronize()
     HF.TIMER.reset()
     HF.TIMER.names = {"render_bwd"}
+    # the roofline's launch time from every 4th timed step (>= 5 launches at the
+    # default 20 steps): an event pair idles the device ~10 us per step it brackets
+    HF.TIMER.every = 4 if args.steps >= 20 else 1
     HF.TIMER.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -271,6 +274,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     HF.TIMER.enabled = False
+    HF.TIMER.every = 1
     HF.L.check_device_faults()                # after the timed region: one blocking read
     t = torch.tensor([dt], device=dev)
     if world > 1:

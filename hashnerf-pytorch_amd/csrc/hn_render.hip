@@ -1716,6 +1716,72 @@ HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], 
 #endif
 constexpr size_t kDcRay = (size_t)kSc * 32 + HN_DC_PAD;
 static_assert(HN_DC_PAD % 4 == 0, "f32x4 alignment");
+// dW(coarse) (+)= sum_b slab[b][0], dW(fine) (+)= sum_b (slab[b][1] +
+// slab[b][2] + slab[b][3]).  64 consecutive elements per block, kSlabGroups
+// slab-groups per element (8 loads in flight per thread, ~18 waves per CU: the
+// read is latency bound otherwise), LDS combine in a fixed order, so the sums
+// are deterministic given the slabs.
+constexpr int kSlabGroups = 16;
+#ifndef HN_SLAB_ILP   // slab loads in flight per thread (a power of 2)
+#define HN_SLAB_ILP 8
+#endif
+constexpr int kSlabIlp = HN_SLAB_ILP;
+// One slab-reduce block's 64 elements (vblock): the arithmetic of every
+// element is fixed (the group partials, then the pairwise combines), so the
+// sums are the same whichever kernel runs it (slab_reduce_kernel, or the
+// binned scatter's tail, HN_SC_SLAB).  1024 threads; part[16][64] in LDS.
+HN_DEV void slab_reduce_block(const float* __restrict__ slab, int n_blocks, const hn_mlp_grad& dc,
+                              const hn_mlp_grad& df, int overwrite, int vblock, float (*part)[64]) {
+  const int lane = threadIdx.x & 63;
+  const int e = vblock * 64 + lane;
+  const int grp = threadIdx.x >> 6;
+  const bool fine = e >= W_END;
+  const int i = fine ? e - W_END : e;
+  // the slabs summed for this element: (block, slot) pairs, slot 0 (coarse)
+  // or 1..3 (fine), flattened
+  const int per = fine ? kSlabSlots - 1 : 1, n_slabs = n_blocks * per;
+  auto slab_at = [&](int q) {
+    const int b = q / per, slot = fine ? 1 + q % per : 0;
+    return slab[((size_t)b * kSlabSlots + slot) * W_END + i];
+  };
+  float s = 0.f;
+  if (e < 2 * W_END) {
+    float acc[kSlabIlp];
+#pragma unroll
+    for (int u = 0; u < kSlabIlp; ++u) acc[u] = 0.f;
+    int q = grp;
+    for (; q + (kSlabIlp - 1) * kSlabGroups < n_slabs; q += kSlabIlp * kSlabGroups)
+#pragma unroll
+      for (int u = 0; u < kSlabIlp; ++u) acc[u] += slab_at(q + kSlabGroups * u);
+    for (; q < n_slabs; q += kSlabGroups) acc[0] += slab_at(q);
+#pragma unroll
+    for (int w = kSlabIlp / 2; w >= 1; w /= 2)   // pairwise, fixed order
+#pragma unroll
+      for (int u = 0; u < w; ++u) acc[u] = acc[u] + acc[u + w];
+    s = acc[0];
+  }
+  part[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && e < 2 * W_END) {
+    float t[kSlabGroups];
+#pragma unroll
+    for (int g = 0; g < kSlabGroups; ++g) t[g] = part[g][lane];
+#pragma unroll
+    for (int w = kSlabGroups / 2; w >= 1; w /= 2)
+#pragma unroll
+      for (int g = 0; g < w; ++g) t[g] = t[g] + t[g + w];
+    s = t[0];
+    const hn_mlp_grad& d = fine ? df : dc;
+    float* dst;
+    if (i < W_S1) dst = d.sigma0 + i;
+    else if (i < W_C0) dst = d.sigma1 + (i - W_S1);
+    else if (i < W_C1) dst = d.color0 + (i - W_C0);
+    else if (i < W_C2) dst = d.color1 + (i - W_C1);
+    else dst = d.color2 + (i - W_C2);
+    *dst = overwrite ? s : *dst + s;
+  }
+}
+constexpr int kSlabVBlocks = (2 * W_END + 63) / 64;
 struct ScK {
   GridArgs g;
   int64_t B;
@@ -1733,7 +1799,16 @@ struct ScK {
   int32_t tv_off[17];
   const float* g_tv;
   TvK tv;
+  // HN_SC_SLAB: the blocks then reduce the MLP backward's dW slabs (the
+  // slab_reduce_kernel launch folded into this one; same per-element sums)
+  const float* slab;       // NULL: no slab reduction here
+  hn_mlp_grad dc, df;
+  int32_t overwrite_mlp;
 };
+#ifndef HN_SC_SLAB       // 1: the binned scatter's blocks also reduce the dW slabs (no slab_reduce launch)
+#define HN_SC_SLAB 1
+#endif
+__device__ unsigned int g_slab_next;   // next slab block for the scatter blocks (HN_SC_SLAB)
 #ifndef HN_SC_PERM       // 1: a block's rays through the backward's batch permutation
 #define HN_SC_PERM 0
 #endif
@@ -2101,6 +2176,23 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     const uint32_t n = lovf < bw.n_ovf ? lovf : bw.n_ovf;
     ob.blk[blockIdx.x] = n;
     if (n) __hip_atomic_fetch_add(ob.cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (k.slab) {   // the dW slabs are complete (the MLP-backward kernel ran before this one)
+    float(*part)[64] = reinterpret_cast<float(*)[64]>(stv);   // the staging pool is free now
+    static_assert(sizeof(stv) >= sizeof(float) * kSlabGroups * 64 && 64 * kScWaves == 64 * kSlabGroups,
+                  "slab-reduce blocks inside the scatter blocks");
+    // the 292 slab blocks go to the scatter blocks as they finish (a counter
+    // reset by render_comp_bwd_kernel): the sums do not depend on who runs them
+    __shared__ int vb_sh;
+    for (;;) {
+      __syncthreads();   // part and vb_sh are free (the pool's last readers, or the previous combine)
+      if (threadIdx.x == 0)
+        vb_sh = (int)__hip_atomic_fetch_add(&g_slab_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int vb = vb_sh;
+      if (vb >= kSlabVBlocks) break;
+      slab_reduce_block(k.slab, kBwdBlocks, k.dc, k.df, k.overwrite_mlp, vb, part);
+    }
   }
 }
 
@@ -2553,6 +2645,7 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
     const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
     uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
     for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
+    if (threadIdx.x == 0) g_slab_next = 0u;   // the scatter kernel's slab-block counter
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -2796,66 +2889,10 @@ void render_bwd_kernel(B1K k) {
 #endif
 }
 
-// dW(coarse) (+)= sum_b slab[b][0], dW(fine) (+)= sum_b (slab[b][1] +
-// slab[b][2] + slab[b][3]).  64 consecutive elements per block, kSlabGroups
-// slab-groups per element (8 loads in flight per thread, ~18 waves per CU: the
-// read is latency bound otherwise), LDS combine in a fixed order, so the sums
-// are deterministic given the slabs.
-constexpr int kSlabGroups = 16;
-#ifndef HN_SLAB_ILP   // slab loads in flight per thread (a power of 2)
-#define HN_SLAB_ILP 8
-#endif
-constexpr int kSlabIlp = HN_SLAB_ILP;
 __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_blocks,
                                                                        hn_mlp_grad dc, hn_mlp_grad df, int overwrite) {
   __shared__ float part[kSlabGroups][64];
-  const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 64 + lane;
-  const int grp = threadIdx.x >> 6;
-  const bool fine = e >= W_END;
-  const int i = fine ? e - W_END : e;
-  // the slabs summed for this element: (block, slot) pairs, slot 0 (coarse)
-  // or 1..3 (fine), flattened
-  const int per = fine ? kSlabSlots - 1 : 1, n_slabs = n_blocks * per;
-  auto slab_at = [&](int q) {
-    const int b = q / per, slot = fine ? 1 + q % per : 0;
-    return slab[((size_t)b * kSlabSlots + slot) * W_END + i];
-  };
-  float s = 0.f;
-  if (e < 2 * W_END) {
-    float acc[kSlabIlp];
-#pragma unroll
-    for (int u = 0; u < kSlabIlp; ++u) acc[u] = 0.f;
-    int q = grp;
-    for (; q + (kSlabIlp - 1) * kSlabGroups < n_slabs; q += kSlabIlp * kSlabGroups)
-#pragma unroll
-      for (int u = 0; u < kSlabIlp; ++u) acc[u] += slab_at(q + kSlabGroups * u);
-    for (; q < n_slabs; q += kSlabGroups) acc[0] += slab_at(q);
-#pragma unroll
-    for (int w = kSlabIlp / 2; w >= 1; w /= 2)   // pairwise, fixed order
-#pragma unroll
-      for (int u = 0; u < w; ++u) acc[u] = acc[u] + acc[u + w];
-    s = acc[0];
-  }
-  part[grp][lane] = s;
-  __syncthreads();
-  if (grp != 0 || e >= 2 * W_END) return;
-  float t[kSlabGroups];
-#pragma unroll
-  for (int g = 0; g < kSlabGroups; ++g) t[g] = part[g][lane];
-#pragma unroll
-  for (int w = kSlabGroups / 2; w >= 1; w /= 2)
-#pragma unroll
-    for (int g = 0; g < w; ++g) t[g] = t[g] + t[g + w];
-  s = t[0];
-  const hn_mlp_grad& d = fine ? df : dc;
-  float* dst;
-  if (i < W_S1) dst = d.sigma0 + i;
-  else if (i < W_C0) dst = d.sigma1 + (i - W_S1);
-  else if (i < W_C1) dst = d.color0 + (i - W_C0);
-  else if (i < W_C2) dst = d.color1 + (i - W_C1);
-  else dst = d.color2 + (i - W_C2);
-  *dst = overwrite ? s : *dst + s;
+  slab_reduce_block(slab, n_blocks, dc, df, overwrite, blockIdx.x, part);
 }
 
 // Owner pass of the binned scatter: workgroup b sums every record of bin b
@@ -3523,6 +3560,10 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
       }
       for (int l = a->tv->n_levels; l <= 16; ++l) sk.tv_off[l] = off;
     }
+    sk.slab = HN_SC_SLAB ? slab : nullptr;
+    sk.dc = a->d_coarse;
+    sk.df = a->d_fine;
+    sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
     hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), 0, s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
@@ -3588,9 +3629,11 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
 #endif
   }
 #endif
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((2 * W_END + 63) / 64), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,
-                     a->d_coarse, a->d_fine, (a->d_table_mode & 2) ? 1 : 0);
-  if ((st = hip_status(hipGetLastError()))) return st;
+  if (mode != kModeSplit || !HN_SC_SLAB) {
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(kSlabVBlocks), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,
+                       a->d_coarse, a->d_fine, (a->d_table_mode & 2) ? 1 : 0);
+    if ((st = hip_status(hipGetLastError()))) return st;
+  }
   if (tv_atomic) return hn_tv_bwd(a->tv, a->g_tv, a->d_table, stream);
   return HN_OK;
 }

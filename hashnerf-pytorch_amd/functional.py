@@ -21,15 +21,22 @@ class KernelTimer:
     recorded on the same stream the kernels are enqueued on.  ``names``
     limits the timed launches (None: all); each recorded event idles the
     device for ~5 us, so bench times only what its line reports from the
-    timed steps."""
+    timed steps.  ``every`` = k times only every k-th call of a name (the
+    sampled launches' mean; the others carry no events)."""
 
     def __init__(self):
         self.events = {}
         self.enabled = False
         self.names = None
+        self.every = 1
+        self.calls = {}
 
     def begin(self, name):
         if not self.enabled or (self.names is not None and name not in self.names):
+            return None
+        c = self.calls.get(name, 0)
+        self.calls[name] = c + 1
+        if c % max(self.every, 1):
             return None
         e = torch.cuda.Event(enable_timing=True)
         e.record()
@@ -48,6 +55,7 @@ class KernelTimer:
 
     def reset(self):
         self.events = {}
+        self.calls = {}
 
 
 TIMER = KernelTimer()

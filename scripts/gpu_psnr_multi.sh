@@ -16,7 +16,7 @@ RC=0
 run_batch() {
   local PIDS=()
   for S in "$@"; do
-    HN_PSNR_SEED=$S HN_PSNR_TAIL=${HN_PSNR_TAIL:-0.2} HN_PSNR_ITERS=5000 HN_PSNR_EVERY=100 HN_PSNR_RES=200 HN_PSNR_NTRAIN=100 HN_PSNR_NTEST=8 \
+    HN_PSNR_SEED=$S HN_PSNR_TAIL=${HN_PSNR_TAIL:-0.2} HN_PSNR_ITERS=5000 HN_PSNR_EVERY=${HN_PSNR_EVERY:-100} HN_PSNR_RES=200 HN_PSNR_NTRAIN=100 HN_PSNR_NTEST=8 \
     HN_PSNR_OUT=$OUT/psnr_5k_${TAG}_seed$S.json OMP_NUM_THREADS=1 \
         timeout -k 10 ${HN_PSNR_TIMEOUT:-540} python -u -m pytest tests/test_psnr.py -q -s -p no:cacheprovider \
         > $OUT/psnr_5k_${TAG}_seed$S.log 2>&1 &
