@@ -2938,6 +2938,9 @@ constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2
 #ifndef HN_BR_PF
 #define HN_BR_PF 0
 #endif
+#ifndef HN_BR_REV
+#define HN_BR_REV 0
+#endif
 static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
 #ifndef HN_BR_DEPTH   // records per thread and fetch group (two groups in flight)
 #define HN_BR_DEPTH 4
@@ -3069,7 +3072,11 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __shared__ uint32_t wsum[kBwdBlocks / 64], wmax[kBwdBlocks / 64];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(acc4);
   const int n4 = (2 << k.shift) / 2;   // f32x4 = 2 accumulators
+#if HN_BR_REV   // the finest levels' (heaviest) bins dispatched first, the light coarse ones fill the tail
+  const uint32_t b = gridDim.x - 1u - blockIdx.x;
+#else
   const uint32_t b = blockIdx.x;
+#endif
   const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
   const int nd4 = (2 << k.shift) / 4;             // float4s of the slice (<= 4 per thread)
   float4 sp[kSliceF4], sm[kSliceF4], sv[kSliceF4];

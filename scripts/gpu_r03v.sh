@@ -34,7 +34,7 @@ echo "chain ok"
 # A/B (one box): the forward's ReLU mask bits through an inline v_min_u32
 # (HN_MASK_ASM=1: 2 VALU per register instead of 3; identical bits)
 for R in 1 2; do
-  for V in base var_maskasm; do
+  for V in base var_maskasm var_brrev; do
     if [ $V = base ]; then unset HN_LIB_PATH; else export HN_LIB_PATH=hashnerf-pytorch_amd/build/$V.so; fi
     timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/ab_${V}_${TAG}_$R.json 2> $OUT/ab_${V}_${TAG}_$R.err || exit 8
     python -c "import json;d=json.load(open('$OUT/ab_${V}_${TAG}_$R.json'));print('$V', d['value'], d['ms_per_step'], d['kernels']['render_fwd_ms'], d['kernels']['render_bwd_ms'])"

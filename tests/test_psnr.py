@@ -134,6 +134,21 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     res = O.level_resolutions(16, 16, args.finest_res)
     T = args.log2_hashmap_size
     ref = _oracle_trainer(O, tr, DEV)
+    # HN_PSNR_REF_CACHE=run.json: the reference path's curve from an earlier
+    # paired run at the same seed and settings.  The reference path is a
+    # function of the seed alone (its initial parameters and every batch come
+    # from the same Trainer streams, and nothing it runs is library code), so
+    # its PSNR at an iteration is the same number on every library version;
+    # only the HIP side is re-run.  (A paired run of the same seed checks this:
+    # scripts/psnr_aggregate.py compares the curves of runs sharing a seed.)
+    cache = None
+    cpath = os.environ.get("HN_PSNR_REF_CACHE")
+    if cpath:
+        cache = json.load(open(cpath))
+        for key, want in (("seed", seed), ("iters", iters), ("H", H), ("W", W), ("n_train", n_train),
+                          ("n_test", n_test), ("N_rand", args.N_rand)):
+            assert cache.get(key) == want, f"reference cache {cpath}: {key} {cache.get(key)} != {want}"
+        cache = {c["iter"]: c["psnr_ref"] for c in cache["curve"]}
     curve = []
     t_hip = t_ref = 0.0
     lr = args.lrate
@@ -144,7 +159,8 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         tr.step(i, batch)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        _oracle_step(O, ref, i, batch, args, box, res, T, lr)
+        if cache is None:
+            _oracle_step(O, ref, i, batch, args, box, res, T, lr)
         torch.cuda.synchronize()
         t_hip += t1 - t0
         t_ref += time.perf_counter() - t1
@@ -152,7 +168,7 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         assert abs(lr - tr.optimizer.param_groups[0]["lr"]) <= 1e-12 * max(lr, 1.0)
         if (i % every == 0 and (i > (1. - tail_frac) * iters or i % (5 * every) == 0)) or i == iters:
             ph, _ = _eval_hip(hn, tr, data)
-            pr, _ = _eval_oracle(O, ref, data, box, res, T)
+            pr = cache[i] if cache is not None else _eval_oracle(O, ref, data, box, res, T)[0]
             curve.append(dict(iter=i, psnr_hip=round(ph, 4), psnr_ref=round(pr, 4),
                               diff=round(ph - pr, 4)))
             print(f"iter {i}: PSNR hip {ph:.3f}  ref {pr:.3f}  diff {ph - pr:+.3f}", flush=True)
@@ -187,6 +203,7 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         stat["hip_other_seeds"] = spread
     tol = TOL_DB_RUN if iters >= 5000 else TOL_DB_SHORT
     out = dict(iters=iters, seed=seed, H=H, W=W, N_rand=args.N_rand, n_train=n_train, n_test=n_test, tail=tail_frac,
+               ref_cache=cpath or None,
                scene="procedural chair (train.procedural_field)", tol_db=tol, final=stat, curve=curve,
                ms_per_iter_hip=round(1e3 * t_hip / iters, 3),
                ms_per_iter_ref_eager_gpu=round(1e3 * t_ref / iters, 3))
