@@ -67,8 +67,9 @@ BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
 N_SIMDS = 1024                   # 256 CUs x 4 SIMDs
 # the kernels of one hn_render_bwd launch, per table-gradient scatter
 BWD_KERNELS = {"atomic": ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel"),
+               # binned: the dW slab reduction runs inside scatter_bins_kernel (HN_SC_SLAB)
                "binned": ("render_comp_bwd_kernel", "render_bwd_kernel", "scatter_bins_kernel",
-                          "ovf_place_kernel", "bin_reduce_kernel", "slab_reduce_kernel")}
+                          "ovf_place_kernel", "bin_reduce_kernel")}
 
 
 def measured_traffic(cfg_id, n_rand_override, scene, pretrain, scatter):

@@ -25,6 +25,10 @@ over paired seeds, PSNR being the median over the evaluations in the last 20 %
 of a run (one evaluation swings with the optimizer's step noise).  HN_PSNR_SEEDS=k adds k HIP-only runs
 at other seeds, to show how far two equally good runs land apart.
 
+HN_PSNR_REF_CACHE=run.json re-runs only the HIP side of a seed against the
+reference curve of an earlier paired run (the reference path depends on the
+seed alone; scripts/gpu_psnr_seq.sh checks it by re-running one seed in full).
+
 The default run is short (HN_PSNR_ITERS, default 400 iterations at 100x100,
 50 views); HN_PSNR_ITERS=5000 HN_PSNR_EVERY=100 HN_PSNR_RES=200
 HN_PSNR_NTRAIN=100 HN_PSNR_OUT=path gives one paired run at 5k iterations
