@@ -80,8 +80,8 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 #ifndef HN_GEMM_TAILNOP
 #define HN_GEMM_TAILNOP 0
 #endif
-#ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk
-#define HN_GEMM_PF 1
+#ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk; 0: at use
+#define HN_GEMM_PF 0  // round 3 (r03ab, one box): render_fwd_kernel 0.324 -> 0.314 ms with 0, same results
 #endif
 #ifndef HN_FRAG_BUF  // 1: fragment groups through frag_load (buffer loads, scalar offsets)
 #define HN_FRAG_BUF 1
