@@ -8,15 +8,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Diagnostic ablations (never set in the product build; scripts/ablate.sh):
-// 1 = no scatter atomics, 2 = no MLP in the render backward (stand-in feature
-// grads are scattered), 3 = no weight
-// gradients (transposes staged, no MFMA / accumulation), 4 = weight-gradient
-// MFMAs without the LDS accumulation.
-#ifndef HN_ABLATE
-#define HN_ABLATE 0
-#endif
-
 #include "../../include/hashnerf_amd.h"
 
 #define HN_DEV __device__ __forceinline__

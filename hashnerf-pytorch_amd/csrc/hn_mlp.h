@@ -75,33 +75,16 @@ enum : int { W_S0 = 0, W_S1 = 2048, W_C0 = 3072, W_C1 = 5056, W_C2 = 9152, W_END
 static_assert(W_END == HN_MLP_PARAMS, "param count");
 
 // acc += A(region R, block ob) . B where bval(s) is the B operand of f32 k-step s.
-// The next A fragments are loaded while the current ones' MFMAs run; the
+// Split-f32: each chunk's A fragments are loaded at use (round 3: loading the
+// next chunk's during the current one's MFMAs measured 0.324 against 0.314 ms
+// for render_fwd_kernel, identical results).  f32: one group ahead.  The
 // scheduling barrier stops hipcc from hoisting all loads (register blowup).
-#ifndef HN_GEMM_TAILNOP
-#define HN_GEMM_TAILNOP 0
-#endif
-#ifndef HN_GEMM_PF   // 1: the next chunk's A fragments are loaded during the current chunk; 0: at use
-#define HN_GEMM_PF 0  // round 3 (r03ab, one box): render_fwd_kernel 0.324 -> 0.314 ms with 0, same results
-#endif
-#ifndef HN_FRAG_BUF  // 1: fragment groups through frag_load (buffer loads, scalar offsets)
-#define HN_FRAG_BUF 1
-#endif
-#ifndef HN_GEMM_SWP  // 1: the next chunk's B split is interleaved with this chunk's MFMAs
-#define HN_GEMM_SWP 0
-#endif
 template <int R, typename BF>
 HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF bval) {
   constexpr int KS = kRegKS[R], NS = reg_ns(R), GPO = reg_gpo(R), OFF = reg_off(R);
-#if HN_FRAG_BUF
   // fragment group g of this block: frag_load (scalar offsets, hn_common.h)
   auto ld = [&](int g) { return frag_load(P, OFF + (ob * GPO + g) * 256, lane); };
-#else
-  // opaque BEFORE the offset: keeps hipcc from precomputing ~50 uniform GEMM
-  // base addresses at the top of the tile loop (SGPR pairs that then spill)
-  const float* base = opaque_ptr(P) + OFF + ob * GPO * 256 + lane * 4;
-  auto ld = [&](int g) { return *reinterpret_cast<const f32x4*>(base + g * 256); };
-#endif
-  if constexpr (NS > 0 && !HN_GEMM_PF) {        // split-f32, fragments loaded at use
+  if constexpr (NS > 0) {        // split-f32, fragments loaded at use
 #pragma unroll
     for (int c = 0; c < KS / 8; ++c) {
       SP<NS> a;
@@ -111,44 +94,6 @@ HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF
       acc = mfma_split<NS>(a, b, acc);
       __builtin_amdgcn_sched_barrier(0);
     }
-    return acc;
-  } else if constexpr (NS > 0) {                // split-f32 on the bf16 MFMA
-    SP<NS> an;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) an.p[q] = as_bf16x8(ld(q));
-#if HN_GEMM_SWP
-    SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
-#endif
-#pragma unroll
-    for (int c = 0; c < KS / 8; ++c) {
-      const SP<NS> a = an;
-      if (c + 1 < KS / 8) {
-#pragma unroll
-        for (int q = 0; q < NS; ++q)
-          an.p[q] = as_bf16x8(ld(NS * (c + 1) + q));
-      }
-#if HN_GEMM_SWP
-      // the next chunk's split (VALU) goes into this chunk's MFMA gaps
-      SP<NS> bn = b;
-      if (c + 1 < KS / 8) bn = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-      acc = mfma_split<NS>(a, b, acc);
-      if (c + 1 < KS / 8) {
-#pragma unroll
-        for (int i = 0; i < (NS == 3 ? 6 : 3); ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, NS == 3 ? 6 : 5, 0);   // then VALU
-        }
-      }
-      b = bn;
-#else
-      const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
-      acc = mfma_split<NS>(a, b, acc);
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#if HN_GEMM_TAILNOP   // diagnostic: 16 extra wait states between a GEMM's last MFMA and any reader
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-#endif
     return acc;
   } else {
     f32x4 an = ld(0);
@@ -171,22 +116,13 @@ struct MlpAct {
   f32x16 c1[2];
   uint32_t m[3];   // ReLU masks of h0, c0, c1 (bit 16 ob + r: value > 0), formed as each is ReLU'd
 };
-#ifndef HN_MASK_ASM
-#define HN_MASK_ASM 0
-#endif
 // mask bits of one ReLU'd D-layout block: its values are +0 or positive, so a
 // bit is (bits + 0x7fffffff) >> 31 (integer ops only: the compare forms, which
 // min(bits, 1) also becomes, hold lane masks in SGPR pairs and spilled the forward)
 HN_DEV void relu_mask_or(const f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-#if HN_MASK_ASM   // v_min_u32 (the compiler turns min(bits, 1) into a compare + select)
-    uint32_t b;
-    asm("v_min_u32 %0, %1, 1" : "=v"(b) : "v"(__float_as_uint(v[r])));
-    m |= b << (16 * ob + r);
-#else
     m |= ((__float_as_uint(v[r]) + 0x7fffffffu) >> 31) << (16 * ob + r);
-#endif
   }
 }
 
@@ -315,17 +251,10 @@ HN_DEV void accum_block(float* acc_lds, int base, int ld, int n0, int nmax, int 
 // One staged weight-gradient block: Tdy/Tx already hold the operands.
 HN_DEV void wgrad_accum(const float* Tdy, const float* Tx, float* Wacc, int base, int ld, int n0,
                         int nmax, int k0, int kmax, int lane) {
-#if HN_ABLATE == 3
-  return;
-#endif
   lds_fence_wave();
   const f32x16 d = wgrad_block(Tdy, Tx, lane);
   lds_fence_wave();
-#if HN_ABLATE == 4
-  if (d[0] == 1234.5f && d[1] == -1234.5f) Wacc[lane] = d[2];
-#else
   accum_block(Wacc, base, ld, n0, nmax, k0, kmax, d, lane);
-#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 

@@ -111,21 +111,15 @@ HN_DEV void ray_point(const Ray& r, float z, float pt[3]) {
 // and the backward's load are fully coalesced dwordx4 accesses.
 // After the 8 feature tiles: the tiles' ReLU masks of the two networks (tile
 // t: 3 words [h0 | c0 | c1] x 64 lanes, bit 16 ob + r = D register r of
-// output block ob of the lane), written by the forward when HN_B1_SMASK.
+// output block ob of the lane), written by the forward.
 constexpr int kTilesPerRay = (kSc + kSf) / 32;
 constexpr int kMaskWordsPerTile = 3 * 64;
 static_assert(kTilesPerRay * (1024 + kMaskWordsPerTile) == HN_RENDER_FEAT_PER_RAY, "feature cache layout");
 
-// HN_B1_SMASK 1: the forward stores its ReLU masks and the backward's forward
-// recompute uses them with 2-part products (HN_SPLIT_R 2): the recomputed
+// The forward stores its ReLU masks and the backward's forward recompute
+// uses them with 2-part products (HN_SPLIT_R 2): the recomputed
 // activations then differ from the forward's by ~2^-17 relative (the dW
 // operands' own precision), but every ReLU decision is the forward's.
-#ifndef HN_B1_SMASK
-#define HN_B1_SMASK 1
-#endif
-#ifndef HN_FWD_DBG
-#define HN_FWD_DBG 0
-#endif
 
 HN_DEV void store_masks(float* __restrict__ base, int64_t ray, int tile, int lane, const uint32_t (&m)[3]) {
   uint32_t* t = reinterpret_cast<uint32_t*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024) +
@@ -160,9 +154,6 @@ HN_DEV void load_feat(const float* __restrict__ base, int64_t ray, int tile, int
 // grid sizes [16][3] staged in LDS (saves 48 SGPRs), then their reciprocals
 constexpr int kGsRcp = 48, kGsLds = 96;
 
-#ifndef HN_CELL_RCP   // 1: cells from cell_floor (hn_common.h) in the forward's encode
-#define HN_CELL_RCP 1
-#endif
 // Hash-encode one point into the 32-feature tile layout (lane half h owns
 // levels tile_level(m, h), m = 0..7).  hash_encoding.py:84-110.
 HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __restrict__ table, const float pt[3], int h,
@@ -178,11 +169,7 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     const float gs[3] = {gsl[3 * l], gsl[3 * l + 1], gsl[3 * l + 2]};
     const float rg[3] = {gsl[kGsRcp + 3 * l], gsl[kGsRcp + 3 * l + 1], gsl[kGsRcp + 3 * l + 2]};
     Voxel v;
-#if HN_CELL_RCP
     voxel_level_rcp(pt, xc, gs, rg, g.bmin, mask, v);
-#else
-    voxel_level(pt, xc, gs, g.bmin, mask, v);
-#endif
     float f0, f1;
     encode_level_off(table, l << g.log2T, v, f0, f1);
     feat[2 * m] = f0;
@@ -213,35 +200,14 @@ HN_DEV void stage_grid_sizes(const GridArgs& g, float* gsl) {
 // LDS per forward wave (floats).
 constexpr int kFZc = 0, kFZsrc = 64, kFZs = 256, kFRaw = 448, kFW = 1216, kFBins = 1280,
               kFCdf = 1344, kFC0 = 1408, kFLds = 1472;
-#ifndef HN_FWD_C0SH   // 1: color_net.0's SH half once per ray and net (LDS seed), not per tile
-#define HN_FWD_C0SH 1
-#endif
 
 #ifndef HN_FWD_WAVES_PER_SIMD
 #define HN_FWD_WAVES_PER_SIMD 4
-#endif
-#ifndef HN_BWD_CHUNK   // 1: each backward block owns a contiguous chunk of the batch
-#define HN_BWD_CHUNK 1
-#endif
-#ifndef HN_BWD_SCRAMBLE   // 1: ... of a pseudo-randomly permuted order of the batch
-#define HN_BWD_SCRAMBLE 1
-#endif
-#ifndef HN_XCD_MAP   // 1: consecutive ray groups of the batch on one XCD (shared L2)
-#define HN_XCD_MAP 1
 #endif
 // 4 waves per SIMD (<= 128 registers; the few spills sit outside the tile
 // loops): one ray per wave, so a 4096-ray batch is exactly one round on 256
 // CUs (3 waves: 0.427 ms, a 1/3-occupied second round; 4: 0.418 ms)
 
-// Diagnostic phase timers of the forward (HN_PROFILE builds): cycles per wave
-// in [0] coarse encode, [1] coarse MLP, [2] composite + sampling + sort,
-// [3] fine encode, [4] fine MLP, [5] final composite, [6] total, [7] waves
-#if HN_PROFILE
-__device__ unsigned long long g_fwd[8];
-#define HN_FT(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); ft[i] += n_ - t_; t_ = n_; } while (0)
-#else
-#define HN_FT(i) ((void)0)
-#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
 void render_fwd_kernel(RenderK k) {
   __shared__ __attribute__((aligned(16))) float smem[kFwdWaves * kFLds + kGsLds];
@@ -251,15 +217,11 @@ void render_fwd_kernel(RenderK k) {
   float* gsl = smem + kFwdWaves * kFLds;
   stage_grid_sizes(k.g, gsl);
   __syncthreads();
-#if HN_XCD_MAP
   // XCD-aware: workgroup b runs on XCD b % 8, so consecutive ray groups of a
   // spatially ordered batch go to one XCD and share its L2
   const int64_t nb = gridDim.x;
   const int64_t grp = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
   const int64_t ray = grp * kFwdWaves + wave;
-#else
-  const int64_t ray = (int64_t)blockIdx.x * kFwdWaves + wave;
-#endif
   if (ray >= k.B) return;
   float* L = smem + wave * kFLds;
   float* zc = L + kFZc;
@@ -271,11 +233,6 @@ void render_fwd_kernel(RenderK k) {
   float* cdf = L + kFCdf;
   Ray r;
   load_ray(k.rays, ray, r);
-#if HN_PROFILE
-  uint64_t ft[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t t0_ = __builtin_amdgcn_s_memtime();
-  uint64_t t_ = t0_;
-#endif
 
   // ---- coarse z_vals (:514-536) ----
   auto zlin = [&](int i) {
@@ -300,10 +257,8 @@ void render_fwd_kernel(RenderK k) {
 
   // ---- coarse network (:540) ----
   float* c0l = L + kFC0;
-#if HN_FWD_C0SH
   c0sh_lds_store(opaque_ptr(k.Pc), sh8, c0l, lane);
   lds_fence_wave();
-#endif
   for (int tau = 0; tau < kSc / 32; ++tau) {
     const float* P = opaque_ptr(k.Pc);
     const int q = 32 * tau + p;
@@ -312,31 +267,15 @@ void render_fwd_kernel(RenderK k) {
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
     if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
-    HN_FT(0);
     MlpAct a;
     f32x16 c2;
-#if HN_FWD_C0SH
-    mlp_fwd_tile_c0<HN_B1_SMASK != 0>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
-#else
-    mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
-#endif
-#if HN_FWD_DBG   // diagnostic: coarse tile 0's sh8 and s1 registers in place of the mask words
-    if (k.feat && tau == 0) {
-      uint32_t* dbg = reinterpret_cast<uint32_t*>(k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dbg[64 * j + lane] = __float_as_uint(sh8[j]);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) dbg[64 * (8 + j) + lane] = __float_as_uint(a.s1[j]);
-    }
-#else
-    if (k.feat) store_masks(k.feat, ray, tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
-#endif
+    mlp_fwd_tile_c0<true>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
+    if (k.feat) store_masks(k.feat, ray, tau, lane, a.m);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
       *reinterpret_cast<float4*>(k.raw_c + (ray * kSc + q) * 4) = o4;
     }
-    HN_FT(1);
   }
   lds_fence_wave();
   CompOut co;
@@ -364,13 +303,10 @@ void render_fwd_kernel(RenderK k) {
   }
   rank_sort_wave(zsrc, zs, kSf, lane, k.fine_src + ray * kSf, kSc);
   for (int i = lane; i < kSf; i += 64) k.z_fine[ray * kSf + i] = zs[i];
-  HN_FT(2);
 
   // ---- fine network (:556) ----
-#if HN_FWD_C0SH
   c0sh_lds_store(opaque_ptr(k.Pf), sh8, c0l, lane);   // the coarse tiles' reads are done (in-order LDS)
   lds_fence_wave();
-#endif
   for (int tau = 0; tau < kSf / 32; ++tau) {
     const float* P = opaque_ptr(k.Pf);
     const int q = 32 * tau + p;
@@ -379,23 +315,15 @@ void render_fwd_kernel(RenderK k) {
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
     if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
-    HN_FT(3);
     MlpAct a;
     f32x16 c2;
-#if HN_FWD_C0SH
-    mlp_fwd_tile_c0<HN_B1_SMASK != 0>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
-#else
-    mlp_fwd_tile<HN_B1_SMASK != 0>(P, feat, sh8, a, c2, lane);
-#endif
-#if !HN_FWD_DBG
-    if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);   // zero words unless HN_B1_SMASK (the cache stays defined)
-#endif
+    mlp_fwd_tile_c0<true>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
+    if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
       *reinterpret_cast<float4*>(k.raw_f + (ray * kSf + q) * 4) = o4;
     }
-    HN_FT(4);
   }
   lds_fence_wave();
   CompOut fo;
@@ -408,13 +336,6 @@ void render_fwd_kernel(RenderK k) {
     k.acc[ray] = fo.acc;
     k.sparsity[ray] = fo.entropy;
   }
-#if HN_PROFILE
-  HN_FT(5);
-  ft[6] = __builtin_amdgcn_s_memtime() - t0_;
-  ft[7] = 1;
-  if (lane == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&g_fwd[i], (unsigned long long)ft[i]);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -442,34 +363,11 @@ constexpr int kB1Img = kMW * kRRows * kXS;                 // floats (112,320 B)
 // Fine-tile hand-off ring (MLP waves -> scatter wave): per slot the tile's
 // feature grads [32 points][kXS] ([f][level], coarse twin added), the 32
 // sample depths and the ray origin / direction.
-#ifndef HN_SLOTS
-#define HN_SLOTS 8
-#endif
-constexpr int kSlots = HN_SLOTS;
+constexpr int kSlots = 8;
 constexpr int kSlotZ = 32 * kXS, kSlotR = kSlotZ + 32, kSlotF = kSlotR + 8;
-// Tile-span runs (HN_TILE_RUNS, scatter_slot): a run of samples in one voxel
-// that crosses from a tile's first 16-point group into its second is issued
-// once, with the second group.  Needs the second group's first cell per
-// level and the held run's values: [16 levels][4] + [16 levels][4 rows][4].
-// Measured off (config 2, procedural after 1000 steps): memory-side atomic
-// requests -5.4 % (20.26 M -> 19.16 M per launch, as scripts/
-// request_model_runs.py predicts) but the backward 1.25 -> 1.32 ms, for any
-// in-flight cap 4..12; the carry's own work without its merges
-// (HN_TILE_RUNS_OFF) costs ~0.01 ms.  The slowdown comes from the merged
-// issue pattern itself, not from the added instructions.
-#ifndef HN_TILE_RUNS
-#define HN_TILE_RUNS 0
-#endif
-constexpr int kCarryF = HN_TILE_RUNS ? 16 * 4 + 16 * 16 : 0;
-constexpr int kVoxF = 16 * 16 * 8 + kCarryF;               // scatter wave's voxel buffer (+ run carry)
-// Compacted atomic issue (HN_COMPACT, scatter_level_x): a ring of kQ {byte
-// offset, value} slots right after the voxel buffer.
-#ifndef HN_COMPACT
-#define HN_COMPACT 0
-#endif
-constexpr int kQ = HN_COMPACT ? 512 : 0;
+constexpr int kVoxF = 16 * 16 * 8;                         // scatter wave's voxel buffer
 constexpr int kSyncInts = 5 + 2 * kSlots;
-constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + 2 * kQ + kGsLds + kSyncInts;
+constexpr int kB1LdsF = kB1Img + kSlots * kSlotF + kVoxF + kGsLds + kSyncInts;
 static_assert(kB1LdsF * 4 <= 160 * 1024, "LDS budget");
 // dW slabs in the workspace: [kBwdBlocks][kSlabSlots][W_END], slot 0 the
 // block's coarse dW, slots 1-3 its fine MLP waves' dW (slab_reduce_kernel)
@@ -545,9 +443,6 @@ HN_DEV bf16x8 img_operand(const char* Xb, int blk, int q, int cc, int lane) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-#ifndef HN_WG_SB   // 0: no scheduling barrier after a weight-gradient chunk (the scheduler may mix it with the next GEMM)
-#define HN_WG_SB 0
-#endif
 // acc[NB * a + b] += sum over the tile's 32 points of A(ablk[a]) B(bblk[b])^T
 // (two K = 16 chunks, 2-part products in mfma_split's order)
 template <int NA, int NB>
@@ -567,9 +462,6 @@ HN_DEV void wgrad_n(const char* Xb, const int (&ablk)[NA], const int (&bblk)[NB]
     for (int ja = 0; ja < NA; ++ja)
 #pragma unroll
       for (int jb = 0; jb < NB; ++jb) acc[NB * ja + jb] = mfma_split<2>(a[ja], b[jb], acc[NB * ja + jb]);
-#if HN_WG_SB
-    __builtin_amdgcn_sched_barrier(0);
-#endif
   }
 }
 
@@ -587,24 +479,15 @@ HN_DEV void wgrad_n(const char* Xb, const int (&ablk)[NA], const int (&bblk)[NB]
 struct GemmSeg {
   int r, ob;   // region (hn_mlp.h), output block; ob = -1: both blocks, chunk by chunk
 };
-#ifndef HN_PAIR_OB   // 1: the two output blocks of a GEMM share one B split (gemm_w2)
-#define HN_PAIR_OB 1
-#endif
-#if HN_PAIR_OB
 constexpr GemmSeg kSegs[] = {{R_F0, -1}, {R_F1, 0}, {R_F2G, -1}, {R_F3, -1}, {R_B4, -1},
                              {R_B3, -1}, {R_B2G, 0}, {R_B1, -1}, {R_B0, 0}};
-#else
-constexpr GemmSeg kSegs[] = {{R_F0, 0}, {R_F0, 1}, {R_F1, 0}, {R_F2G, 0}, {R_F2G, 1}, {R_F3, 0}, {R_F3, 1},
-                             {R_B4, 0}, {R_B4, 1}, {R_B3, 0}, {R_B3, 1}, {R_B2G, 0}, {R_B1, 0}, {R_B1, 1},
-                             {R_B0, 0}};
-#endif
 constexpr int kNSegs = sizeof(kSegs) / sizeof(kSegs[0]);
 // HN_SPLIT_R: parts the backward's forward recompute uses of the forward
 // regions' HN_SPLIT_F packed parts (the leading parts of a split are the same
 // for every part count, so the recompute streams only groups q < HN_SPLIT_R of
 // each chunk).  3 = the forward's own products (bit-identical activations).
 #ifndef HN_SPLIT_R
-#define HN_SPLIT_R (HN_B1_SMASK ? 2 : 3)
+#define HN_SPLIT_R 2
 #endif
 constexpr int seg_ns(const GemmSeg& g) {   // parts this stream uses per chunk (0: f32)
   return g.r < R_B4 && reg_ns(g.r) > HN_SPLIT_R ? HN_SPLIT_R : reg_ns(g.r);
@@ -648,16 +531,9 @@ struct WRing {
 };
 
 // Weight-fragment group load: frag_load (hn_common.h, raw buffer load with a
-// scalar offset); HN_WBUF 0 = the former global load of base + group + lane.
-#ifndef HN_WBUF
-#define HN_WBUF 1
-#endif
+// scalar offset).
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
-#if HN_WBUF
   return frag_load(P, off, lane);
-#else
-  return *reinterpret_cast<const f32x4*>(opaque_ptr(opaque_ptr(P) + off) + 4 * lane);
-#endif
 }
 template <int I, int N, typename F>
 HN_DEV void static_for(F&& f) {
@@ -683,22 +559,13 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
   return a;
 }
 
-// HN_B1_SWP 1: the next chunk's B split (VALU) is issued in the gaps of this
+// The next chunk's B split (VALU) is issued in the gaps of this
 // chunk's MFMAs (sched_group_barrier: one MFMA, then V VALU) instead of after
 // them; the same splits and the same MFMA order, so results are unchanged.
 // Measured (r03g, config 2, two runs each on one box): backward launch
 // 0.812 -> 0.789 ms, step 1.159 -> 1.134 ms; the kernel's 24 VGPR spills go to 0.
-// The same pipelining in the forward's gemm (HN_GEMM_SWP, hn_mlp.h) changed
+// The same pipelining in the forward's gemm (round 3, removed) changed
 // nothing there (render_fwd 0.304 ms either way).
-#ifndef HN_B1_SWP
-#define HN_B1_SWP 1
-#endif
-#ifndef HN_SWP_V3   // VALU per MFMA gap, paired 3-part chunk (12 MFMAs; its split is ~36 VALU)
-#define HN_SWP_V3 3
-#endif
-#ifndef HN_SWP_V2   // VALU per MFMA gap, paired 2-part chunk (6 MFMAs; ~20 VALU)
-#define HN_SWP_V2 4
-#endif
 template <int NMFMA, int NVALU>
 HN_DEV void swp_pattern() {
   static_for<0, NMFMA>([&](auto) {
@@ -714,7 +581,7 @@ template <int SEG, int IMG = -1, int F4B = 0, typename BF>
 HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, char* Xb = nullptr) {
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
-  if constexpr (NS > 0 && HN_B1_SWP && KS > 8) {   // split-f32, next chunk's split in the MFMA gaps
+  if constexpr (NS > 0 && KS > 8) {   // split-f32, next chunk's split in the MFMA gaps
     constexpr int NC = KS / 8;
     SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
     __builtin_amdgcn_sched_barrier(0);
@@ -765,7 +632,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(kSegs[SEG].ob < 0, "paired segment");
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
-  if constexpr (NS > 0 && HN_B1_SWP && KS > 8) {
+  if constexpr (NS > 0 && KS > 8) {
     constexpr int NC = KS / 8;
     SP<NS> b = splitn<NS>([&](int j) { return bval(j); });
     __builtin_amdgcn_sched_barrier(0);
@@ -784,7 +651,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? HN_SWP_V3 : HN_SWP_V2>();
+        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : 4>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -838,46 +705,27 @@ HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, ch
   }
 }
 
-// ReLU with its mask bits.  HN_MASK_INT: integer forms that keep no lane masks
+// ReLU with its mask bits, in integer forms that keep no lane masks
 // live (the compare forms held 16+ SGPR-pair masks across the GEMMs and
 // spilled them to VGPR lanes): relu = the bits with the sign-extended sign
 // cleared (v > 0 ? v : 0 for every non-NaN v, -0 -> +0), bit = relu > 0 from
 // the relu's bits, and the gradient masked by AND with the sign-extended bit.
 // (No inline asm here: an asm operand that is an MFMA result gets none of the
 // MFMA-to-VALU wait states the compiler inserts for its own instructions.)
-#ifndef HN_MASK_INT
-#define HN_MASK_INT 1
-#endif
-#ifndef HN_MASK_MIN
-#define HN_MASK_MIN 1
-#endif
 HN_DEV void relu_bits(f32x16& v, uint32_t& m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-#if HN_MASK_INT
     const uint32_t b = __float_as_uint(v[r]);
     const uint32_t u = b & ~(uint32_t)((int32_t)b >> 31);
-#if HN_MASK_MIN   // bit = min(u, 1): v_min_u32 + v_lshl_or_b32 per element
     m |= min(u, 1u) << (16 * ob + r);
-#else
-    m |= ((u + 0x7fffffffu) >> 31) << (16 * ob + r);
-#endif
     v[r] = __uint_as_float(u);
-#else
-    m |= (v[r] > 0.f ? 1u : 0u) << (16 * ob + r);
-    v[r] = v[r] > 0.f ? v[r] : 0.f;
-#endif
   }
 }
 HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-#if HN_MASK_INT
     const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)m, 16 * ob + r, 1);   // 0 or ~0
     g[r] = __uint_as_float(__float_as_uint(g[r]) & keep);
-#else
-    g[r] = (m >> (16 * ob + r)) & 1u ? g[r] : 0.f;
-#endif
   }
 }
 
@@ -885,38 +733,23 @@ HN_DEV void mask_bits(f32x16& g, uint32_t m, int ob) {
 // tile.  The LDS unit executes one wave's ds instructions in order, so a read
 // issued after a write sees it (also another lane's) and a write after a read
 // does not overwrite what the read returns: only the compiler must keep the
-// program order (HN_B1_LDS_ORDER 1: a compiler barrier; the reads' own
-// lgkmcnt waits stay).  0: s_waitcnt lgkmcnt(0) at each hand-over
-// (lds_fence_wave), which also waits for every write still in flight.
-#ifndef HN_B1_LDS_ORDER
-#define HN_B1_LDS_ORDER 1
-#endif
+// program order: a compiler barrier (the reads' own lgkmcnt waits stay)
+// instead of s_waitcnt lgkmcnt(0) at each hand-over (lds_fence_wave), which
+// also waits for every write still in flight (measured equal, round 3).
 HN_DEV void tile_lds_order() {
-#if HN_B1_LDS_ORDER
   asm volatile("" ::: "memory");
-#else
-  lds_fence_wave();
-#endif
 }
 
 // color_net.0 applied to the ray's sh features (the same for every point of
-// the ray): HN_C0SH_LDS 1 keeps its 64 rows in the wave's LDS slab after the
+// the ray): its 64 rows are kept in the wave's LDS slab after the
 // images (read back as the c0 accumulators' seed, 8 broadcast ds_read_b128
 // per tile) instead of 32 VGPRs live across the unit's tiles.
-#ifndef HN_C0SH_LDS
-#define HN_C0SH_LDS 1
-#endif
 constexpr int kC0shF = kNImg * kImgBlk / 4;   // float offset in the wave's slab
 static_assert(kC0shF + 64 <= kRRows * kXS, "c0sh fits the per-wave slab");
 struct C0Sh {
-#if HN_C0SH_LDS
   const float* lds;
-#else
-  f32x16 v[2];
-#endif
 };
 HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
-#if HN_C0SH_LDS
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
@@ -925,65 +758,23 @@ HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) c0[ob][4 * g + j] = v[j];
     }
-#else
-  (void)h;
-  c0[0] = c.v[0];
-  c0[1] = c.v[1];
-#endif
 }
 
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
-// after_fwd(): called once the forward recompute is done (its activations
-// live on only as LDS images and mask bits) -- where the next unit's prefetch
-// adds the fewest live registers.
-// HN_TILE_PROF (diagnostic, with HN_PROFILE): shader-clock cycles of the
-// tile's segments summed over all tiles (lane 0 of each wave; the stamps cost
-// ~10 % themselves): [0] F0 [1] F1 + F2G [2] F3 + c1 image [3] dW c2 + B4 [4] B3
-// + dW c1 [5] B2G + dW c0 [6] B1 + dW s1 [7] B0 + dW s0
-#ifndef HN_TILE_PROF
-#define HN_TILE_PROF 0
-#endif
-#if HN_TILE_PROF
-__device__ unsigned long long g_tile[9];
-#define HN_TSTAMP(i) do { __builtin_amdgcn_sched_barrier(0); const uint64_t n_ = __builtin_amdgcn_s_memtime(); \
-    if (i >= 0 && lane == 0) atomicAdd(&g_tile[(i) < 0 ? 8 : (i)], (unsigned long long)(n_ - t_ts)); t_ts = n_; \
-    __builtin_amdgcn_sched_barrier(0); } while (0)
-#else
-#define HN_TSTAMP(i) ((void)0)
-#endif
-#ifndef HN_B1_LANE_OPAQUE   // 0: the image addresses may be kept across tiles (registers permitting)
-#define HN_B1_LANE_OPAQUE 1
-#endif
-template <typename AfterFwd>
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
-                      const C0Sh& c0sh, float4 dr, DW& dw, const uint32_t (&sm)[3], AfterFwd&& after_fwd) {
-#if HN_B1_LANE_OPAQUE
+                      const C0Sh& c0sh, float4 dr, DW& dw, const uint32_t (&sm)[3]) {
   const int lane = lane_id();   // opaque: lane-derived LDS addresses are not hoisted out of the loop
-#else
-  const int lane = (int)__lane_id();
-#endif
   const int h = lane >> 5;
   char* Xb = reinterpret_cast<char*>(X);
-#if HN_B1_SMASK   // the forward's ReLU masks (the recompute's own bits go to a dead word)
   uint32_t mh0 = sm[0], mc0 = sm[1], mc1 = sm[2], mdead = 0;
 #define HN_RELU(v, m, ob) relu_bits(v, mdead, ob)
-#else
-  (void)sm;
-  uint32_t mh0 = 0, mc0 = 0, mc1 = 0;
-#define HN_RELU(v, m, ob) relu_bits(v, m, ob)
-#endif
-#if HN_TILE_PROF
-  uint64_t t_ts = 0;
-  HN_TSTAMP(-1);
-#endif
   // ---- forward recompute (models.py:151-174); each GEMM stages its B
   // operand's parts as a dW operand image ----
   f32x16 h0[2] = {zero16(), zero16()};
   gemm2<R_F0, kBF>(wr, P, h0, lane, [&](int s) { return feat[s]; }, Xb);
   HN_RELU(h0[0], mh0, 0);
   HN_RELU(h0[1], mh0, 1);
-  HN_TSTAMP(0);
   const f32x16 s1 = gemm_w<seg_of(R_F1), kBH0>(wr, P, zero16(), lane, [&](int s) { return h0[s >> 4][s & 15]; }, Xb);
   f32x16 c0[2];
   c0sh_seed(c0sh, c0, h);
@@ -991,7 +782,6 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   gemm2<R_F2G, kBC0in, 4>(wr, P, c0, lane, [&](int s) { return s1[s]; }, Xb);
   HN_RELU(c0[0], mc0, 0);
   HN_RELU(c0[1], mc0, 1);
-  HN_TSTAMP(1);
   {
     f32x16 c1[2] = {zero16(), zero16()};
     gemm2<R_F3, kBC0>(wr, P, c1, lane, [&](int s) { return c0[s >> 4][s & 15]; }, Xb);
@@ -1008,9 +798,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
       put_quad(Xb, kBDR, q, lane & 31, 0, w[0], w[1]);
     }
   }
-  after_fwd();
   tile_lds_order();
-  HN_TSTAMP(2);
   // ---- color_net.2 (dW rows >= 3 are discarded) ----
   {
     const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
@@ -1021,7 +809,6 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   gemm2<R_B4>(wr, P, dc1, lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
   mask_bits(dc1[0], mc1, 0);
   mask_bits(dc1[1], mc1, 1);
-  HN_TSTAMP(3);
   // ---- color_net.1 (dc1 image over c1) ----
   f32x16 dc0[2] = {zero16(), zero16()};
   gemm2<R_B3, kBC1>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; }, Xb);
@@ -1032,7 +819,6 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     const int ab[2] = {kBC1, kBC1 + 1}, bb[2] = {kBC0, kBC0 + 1};
     wgrad_n<2, 2>(Xb, ab, bb, dw.c1, lane);     // dw.c1[2 * nb + kb]
   }
-  HN_TSTAMP(4);
   // ---- color_net.0 (dc0 image over c0; B = [sh16 | sigma | geo15]) ----
   f32x16 ds1 = gemm_w<seg_of(R_B2G), kBC0>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; }, Xb);
   if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
@@ -1041,7 +827,6 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBC0in};
     wgrad_n<2, 1>(Xb, ab, bb, dw.c0, lane);
   }
-  HN_TSTAMP(5);
   // ---- sigma_net.1 (ds1 image over dc1's first tile; rows 16..31 discarded) ----
   f32x16 dh0[2] = {zero16(), zero16()};
   gemm2<R_B1, kBC1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; }, Xb);
@@ -1052,7 +837,6 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     const int ab[1] = {kBC1}, bb[2] = {kBH0, kBH0 + 1};
     wgrad_n<1, 2>(Xb, ab, bb, dw.s1, lane);
   }
-  HN_TSTAMP(6);
   // ---- sigma_net.0 (dh0 image over dc0) ----
   const f32x16 dfeat =
       gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; }, Xb);
@@ -1065,10 +849,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     (void)wring_take<decltype(gc)::value>(wr, P, lane);                 // aligned with the tile
   });
   tile_lds_order();                             // image reads done before any later writes
-  HN_TSTAMP(7);
-#if HN_B1_SMASK
   (void)mdead;
-#endif
 #undef HN_RELU
   return dfeat;
 }
@@ -1103,44 +884,16 @@ template <int D> constexpr int kRowShl = 0x100 + D;   // lane i <- lane i+D with
 
 // Voxel of one (point, level) for the scatter: cell corner index and
 // trilinear weights in the op order of hash_encoding.py:62-72 / :130-140.
-#ifndef HN_FAST_VOXEL
-#define HN_FAST_VOXEL 0
-#endif
 HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], const float xc[3], int l,
                      int32_t cell[3], float w[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const float gs = gsl[3 * l + a];
-#if HN_FAST_VOXEL
-    // The cell must be the forward's: floor of the IEEE quotient (x-min)/g.
-    // (x-min) * RN(1/g) is within 2^-23 relative of it, i.e. within 1.3e-4
-    // cells for q <= 1024, so its floor is the quotient's unless the
-    // fraction lies within 2^-10 of an integer: only then (~0.2% of lanes)
-    // the IEEE division is redone.  The weights only scale the gradient:
-    // v_rcp_f32 (1 ulp) instead of the IEEE division moves them by ~2 ulp
-    // (gradient tolerance rtol 1e-4); the forward's weights stay exact.
-    // Measured: no gain (backward 1.267 ms vs 1.256 ms with the IEEE
-    // divisions): the scatter wave's VALU hides under its atomic stalls, so
-    // it stays off.
-    const float num = xc[a] - g.bmin[a];
-    float q = num * gsl[kGsRcp + 3 * l + a];
-    float fq = floorf(q);
-    const float fr = q - fq;
-    if (fr < 0x1p-10f || fr > 1.f - 0x1p-10f) {
-      q = num / gs;
-      fq = floorf(q);
-    }
-    const int32_t i = (int32_t)fq;
-    const float vmin = (float)i * gs + g.bmin[a];
-    const float vmax = vmin + gs;
-    w[a] = (pt[a] - vmin) * __builtin_amdgcn_rcpf(vmax - vmin);
-#else
     const float q = (xc[a] - g.bmin[a]) / gs;   // exact IEEE divisions
     const int32_t i = (int32_t)floorf(q);
     const float vmin = (float)i * gs + g.bmin[a];
     const float vmax = vmin + gs;
     w[a] = (pt[a] - vmin) / (vmax - vmin);
-#endif
     cell[a] = i;
   }
 }
@@ -1153,12 +906,6 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 // 1: 1.59 ms, 2: 1.56, 4: 1.496, 6: 1.508.  With the split-f32 MLP and
 // Morton-ordered batches (scripts/variants_env.sh, two runs each): 4: 1.282 /
 // 1.278 ms, 8: 1.258 / 1.252, 12: 1.275 / 1.274.
-#ifndef HN_NMERGE
-#define HN_NMERGE 0
-#endif
-#ifndef HN_SPLIT_INSTR
-#define HN_SPLIT_INSTR 0
-#endif
 #ifndef HN_SW_VMCNT
 #define HN_SW_VMCNT 8
 #endif
@@ -1171,64 +918,11 @@ HN_DEV void voxel_cw(const GridArgs& g, const float* gsl, const float pt[3], con
 // point's voxel {cell x, cell y * PY, cell z * PZ, w x, y, z} from the compact
 // pass (the prime products are precomputed there: (c + 1) * P = c * P + P,
 // and c -> c * P is a bijection, so run heads compare the products).
-// Compacted issue queue of the scatter wave: head / tail are wave-uniform
-// running counts of slots read / written.  Full 64-slot batches are read
-// into registers after a level's queue writes and issued as atomics at the
-// start of the next level, so the LDS read latency hides under that level's
-// VALU work instead of stalling the wave.
-struct AQ {
-  float2* buf;
-  uint32_t head, tail;
-  uint32_t nb;      // batches held in e[]
-  float2 e[4];
-  uint64_t cap_wait;   // HN_PROFILE: cycles spent waiting on the in-flight cap
-};
-#ifndef HN_QCAP   // compacted atomic wave-instructions in flight before the next is issued
-#define HN_QCAP 4
-#endif
-HN_DEV void aq_atomic(float* __restrict__ dtable, float2 e, bool on) {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HN_QCAP) : "memory");
-  if (on) atomic_add_f32(reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) + __float_as_uint(e.x)), e.y);
-}
-// issue the batches read earlier
-HN_DEV void aq_flush_regs(float* __restrict__ dtable, AQ& q) {
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-    if ((uint32_t)b < q.nb) aq_atomic(dtable, q.e[b], true);
-  q.nb = 0;
-}
-// read every full batch now in the queue (at most 4: a level adds <= 256 slots)
-HN_DEV void aq_read(AQ& q, int lane) {
-  asm volatile("" ::: "memory");                 // after the queue writes (LDS is in order per wave)
-  const uint32_t n = (q.tail - q.head) >> 6;
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-    if ((uint32_t)b < n) q.e[b] = q.buf[(q.head + 64u * (uint32_t)b + (uint32_t)lane) & (uint32_t)(kQ - 1)];
-  q.head += 64u * n;
-  q.nb = n;
-}
-// end of the stream: everything still held or queued
-HN_DEV void aq_drain(float* __restrict__ dtable, AQ& q, int lane) {
-  aq_flush_regs(dtable, q);
-  aq_read(q, lane);
-  aq_flush_regs(dtable, q);
-  const uint32_t n = q.tail - q.head;
-  if (n) {
-    asm volatile("" ::: "memory");
-    const float2 e = q.buf[(q.head + (uint32_t)lane) & (uint32_t)(kQ - 1)];
-    aq_atomic(dtable, e, (uint32_t)lane < n);
-    q.head += n;
-  }
-}
-
 template <int CAP>   // in-flight atomic cap: HN_SW_VMCNT, or HN_SW_VMCNT_BIG for a table beyond the MALL
 HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const f32x4 v0, const float2 v1,
-                            uint32_t l, float gl, int lane, AQ& aq,
-                            [[maybe_unused]] bool hold = false,
-                            [[maybe_unused]] bool take = false, [[maybe_unused]] f32x4 carry_in = {},
-                            [[maybe_unused]] float* carry_out = nullptr) {
+                            uint32_t l, float gl, int lane) {
   const int pp = lane & 15, xi = lane >> 5;
-  [[maybe_unused]] const int f = (lane >> 4) & 1;
+  const int f = (lane >> 4) & 1;
   const uint32_t cx = (uint32_t)__float_as_int(v0.x), y0 = (uint32_t)__float_as_int(v0.y),
                  z0 = (uint32_t)__float_as_int(v0.z);
   const float w[3] = {v0.w, v1.x, v1.y};
@@ -1271,170 +965,23 @@ HN_DEV void scatter_level_x(const GridArgs& g, float* __restrict__ dtable, const
     }
   };
   seg_sum(cv);
-  bool issue = head;
-#if HN_TILE_RUNS
-  // take: this group's first run continues the previous group's last one,
-  // whose sums (rows c = 0..3 of this lane's x/feature) arrive in carry_in;
-  // hold: this group's last run continues into the next group, so its head
-  // parks its sums at carry_out instead of issuing them
-  static_assert(!HN_NMERGE && !HN_COMPACT, "the tile-span carry is wired into the row-per-instruction scatter only");
-  if (take && pp == 0) {
-    cv[0] += carry_in.x; cv[1] += carry_in.y; cv[2] += carry_in.z; cv[3] += carry_in.w;
-  }
-  if (hold && pp == 31 - __builtin_clz(pm)) {
-    *reinterpret_cast<f32x4*>(carry_out) = f32x4{cv[0], cv[1], cv[2], cv[3]};
-    issue = false;
-  }
-#endif
-  // Neighbour merge: consecutive run heads along the ray are usually
-  // adjacent voxels.  After a y/z step a head shares the corner rows (register
-  // c = 2j+k, both x lanes) of the common face with the previous head.  Heads
-  // with an odd index give those rows to the previous head, which has an even
-  // index and never gives, so no contribution is ever passed on twice.  The
-  // previous run's cell is the previous lane's (q0..q2); the given values move
-  // one lane down (into the receiver's run) and a second segmented sum brings
-  // them to the receiving head: DPP only, no LDS round trips.  -15 % memory-
-  // side requests on recorded samples (scripts/request_model.py).
-  uint32_t gfin = 0u;   // rows this lane gives away
-#if HN_NMERGE
-  {
-    const uint32_t hidx = (uint32_t)__builtin_popcount(pm & ((1u << pp) - 1u));
-    const uint32_t yp = y0 - q1 == kPrimeY, ym = q1 - y0 == kPrimeY;
-    const uint32_t zp = z0 - q2 == kPrimeZ, zm = q2 - z0 == kPrimeZ;
-    const bool ystill = y0 == q1, zstill = z0 == q2;
-    const bool yz = head && (hidx & 1u) && cx == q0 && (ystill || yp || ym) && (zstill || zp || zm) &&
-                    !(ystill && zstill);
-    // rows given: j = 0 after +y (my j=0 face is its j=1 face), j = 1 after -y
-    const uint32_t jm = 3u - 2u * yp - ym, km = 3u - 2u * zp - zm;
-    gfin = yz ? (km * (jm & 1u) | (km << 2) * (jm >> 1)) : 0u;
-    // the receiver's row c = (j, k) takes my row (j - dy, k - dz), i.e. row
-    // c ^ (2 [dy != 0] + [dz != 0]) when that is a given row: two selects, no
-    // index arithmetic (a select chain on an index becomes branches)
-    float s1[4], t[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s1[c] = (zp | zm) ? cv[c ^ 1] : cv[c];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float v = (yp | ym) ? s1[c ^ 2] : s1[c];
-      const uint32_t j = (uint32_t)c >> 1, kk = (uint32_t)c & 1u;
-      // receiver row valid: after +y only its j=1 row, after -y only j=0
-      const bool ok = yz && (yp ? j == 1u : (ym ? j == 0u : true)) && (zp ? kk == 1u : (zm ? kk == 0u : true));
-      t[c] = dpp_f<kRowShl<1>>(ok ? v : 0.f);  // into the last lane of the receiver's run
-    }
-    seg_sum(t);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) cv[c] = cv[c] + t[c];
-  }
-#endif
-#if HN_ABLATE == 1   // diagnostic build: everything but the scatter atomics
-  if (cv[0] == 1234.5f && cv[1] == -1234.5f) dtable[lane] = cv[2];
-#elif HN_COMPACT
-  // Compacted issue: the run heads' adds are queued densely in LDS and go out
-  // as full 64-lane atomic wave-instructions across levels, tiles and rays
-  // (coarse levels have 1-3 heads per 16 points: one instruction per corner
-  // row per level carried only 4-12 active lanes).  Queue order: corner row
-  // c, head rank r, lane-in-unit s = 2 xi + f -> slot 4 nh c + 4 r + s, so a
-  // head's x-pair and both features stay adjacent (one 64-B segment) and the
-  // queue writes of one row are consecutive (conflict-free).
-  static_assert(!HN_NMERGE, "the neighbour merge is not wired into the compacted queue");
-  (void)gfin;
-  {
-    aq_flush_regs(dtable, aq);                   // the batches read at the previous level
+  if (head) {
     const uint32_t row0 = l << g.log2T;
-    const uint32_t nh = (uint32_t)__builtin_popcount(pm);
-    if (head) {
-      const uint32_t rk = (uint32_t)__builtin_popcount(pm & ((1u << pp) - 1u));
-      const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
-                              (hx ^ y1 ^ z1) & mask};
-      const uint32_t base = aq.tail + 4u * rk + (uint32_t)(lane >> 4);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        aq.buf[(base + 4u * nh * (uint32_t)c) & (uint32_t)(kQ - 1)] =
-            make_float2(__uint_as_float((row0 + hh[c]) * 8u + 4u * (uint32_t)f), cv[c]);
-    }
-    aq.tail += 16u * nh;
-    aq_read(aq, lane);
-  }
-#else
-#ifdef HN_SKIP_LEVELS   // diagnostic: no atomics for the levels in this mask (wrong gradients)
-  if ((HN_SKIP_LEVELS >> l) & 1u) issue = false;
-#endif
-  if (issue) {
-    const uint32_t row0 = l << g.log2T;
-#ifdef HN_DIAG_REP   // diagnostic: levels < HN_DIAG_REP spread over 8 row-shifted copies (wrong gradients)
-    const uint32_t sh_ = l < HN_DIAG_REP ? (blockIdx.x & 7u) << 16 : 0u;
-    const uint32_t hh[4] = {((hx ^ y0 ^ z0) + sh_) & mask, ((hx ^ y0 ^ z1) + sh_) & mask,
-                            ((hx ^ y1 ^ z0) + sh_) & mask, ((hx ^ y1 ^ z1) + sh_) & mask};
-#else
     const uint32_t hh[4] = {(hx ^ y0 ^ z0) & mask, (hx ^ y0 ^ z1) & mask, (hx ^ y1 ^ z0) & mask,
                             (hx ^ y1 ^ z1) & mask};
-#endif
-#if HN_SW_VMCNT >= 0
     // cap the atomics in flight (they share the CU's vector-memory pipeline
     // with the MLP waves' weight loads); waiting only here, after this
     // level's VALU, overlaps the wait with it
-#if HN_PROFILE
-    const uint64_t tw_ = __builtin_amdgcn_s_memtime();
-#endif
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CAP) : "memory");
-#if HN_PROFILE
-    aq.cap_wait += __builtin_amdgcn_s_memtime() - tw_;
-#endif
-#endif
-#if HN_SPLIT_INSTR   // diagnostic: the same requests in twice the wave-instructions
-    for (int half = 0; half < 2; ++half) {
-      if ((pp >> 3) == half) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if ((gfin >> c) & 1u) continue;
-          float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
-                                                (row0 + hh[c]) * 8u + 4u * f);
-          atomic_add_f32(dst, cv[c]);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#else
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if ((gfin >> c) & 1u) continue;           // given to the previous head
       float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(dtable) +
                                             (row0 + hh[c]) * 8u + 4u * f);
       atomic_add_f32(dst, cv[c]);
     }
-#endif
   }
-#endif
 }
 
-// Diagnostic phase timers (HN_PROFILE builds only, scripts/b1_profile.sh):
-// per wave, shader-clock cycles spent in the unit prologue (composite
-// backward, sh, loads), in MLP tiles and in scatter tiles.
-#ifndef HN_PROFILE
-#define HN_PROFILE 0
-#endif
-struct PhaseClock {
-#if HN_PROFILE
-  uint64_t t = 0, unit = 0, mlp = 0, scat = 0, tiles = 0;
-  HN_DEV void start() { t = __builtin_amdgcn_s_memtime(); }
-  HN_DEV void lap(uint64_t& acc) {
-    const uint64_t n = __builtin_amdgcn_s_memtime();
-    acc += n - t;
-    t = n;
-  }
-#else
-  HN_DEV void start() {}
-#endif
-};
-#if HN_PROFILE
-#define HN_LAP(pc, field) (pc).lap((pc).field)
-__device__ unsigned long long g_phase[2][8];
-// ring waits: [0] scatter wave total, [1] scatter wave waiting on ready,
-// [2] MLP waves waiting on a free slot, [3] MLP waves waiting on the coarse flag
-__device__ unsigned long long g_ring[5];   // [4] scatter wave waiting on the atomic cap
-#else
-#define HN_LAP(pc, field) ((void)0)
-#endif
 
 
 // ---- fine-tile hand-off ring ----------------------------------------------
@@ -1450,7 +997,6 @@ __device__ unsigned long long g_ring[5];   // [4] scatter wave waiting on the at
 struct Ring {
   float* slots;
   int* tick;    // next ticket
-  int* selfc;   // tiles an MLP wave scattered itself (ring full)
   int* ready;   // [kSlots] ticket + 1 of the slot's contents
   int* freed;   // [kSlots] times consumed
   const float* gsl;
@@ -1468,9 +1014,6 @@ HN_DEV void raise_fault(int bit) {
 
 // Bounded spin on a workgroup-local flag.
 HN_DEV void spin_until(int* flag, int need, int fault_bit, int prof_slot = -1) {
-#if HN_PROFILE
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
-#endif
   bool ok = false;
   for (int it = 0; it < kSpinCap; ++it) {
     const int v = __builtin_amdgcn_readfirstlane(
@@ -1483,10 +1026,6 @@ HN_DEV void spin_until(int* flag, int need, int fault_bit, int prof_slot = -1) {
   }
   if (!ok) raise_fault(fault_bit);
   asm volatile("" ::: "memory");
-#if HN_PROFILE
-  if (prof_slot >= 0 && lane_id() == 0)
-    atomicAdd(&g_ring[prof_slot], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
-#endif
 }
 
 HN_DEV int lds_load(int* p) {
@@ -1556,19 +1095,16 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
 // dropping the contribution.
 enum : int { kFaultBins = 16, kFaultNonFinite = 32, kFaultDeadRow = 64 };
 
-// Record r in memory.  HN_REC_AOS 0 (default): the values [nrec] f32x4 then
-// the words [nrec] u32.  HN_REC_AOS 1: groups of 4 records = 4 value quads
+// Record r in memory: the values [nrec] f32x4 then the words [nrec] u32.
+// Measured and removed (round 2): groups of 4 records = 4 value quads
 // then their 4 entry words (80 B), a record's value and word in one line and
 // one write stream per region -- measured slower on config 2 (scatter +5 us,
 // owner +6.5 us, two A/B pairs on one box): the owner's value loads then span
 // 80-B strides instead of dense 1-KiB runs.  Either way the records take
 // 5 * nrec floats from `bins` and the book words follow at bins + 5 * nrec
 // (ovf_book's idx base = bins + 4 * nrec).
-#ifndef HN_REC_AOS
-#define HN_REC_AOS 0
-#endif
-HN_DEV size_t rec_vofs(size_t r) { return HN_REC_AOS ? (r >> 2) * 20 + (r & 3) * 4 : 4 * r; }
-HN_DEV size_t rec_wofs(size_t r, size_t nrec) { return HN_REC_AOS ? (r >> 2) * 20 + 16 + (r & 3) : 4 * nrec + r; }
+HN_DEV size_t rec_vofs(size_t r) { return 4 * r; }
+HN_DEV size_t rec_wofs(size_t r, size_t nrec) { return 4 * nrec + r; }
 struct BinW {
   float* bins;
   size_t nrec;
@@ -1648,11 +1184,7 @@ HN_DEV RecSlot rec_slot(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx,
   RecSlot r;
   r.word = flat | (nbits << 28);
   r.bin = flat >> bw.shift;
-#if HN_SC_DIAG == 2   // diagnostic: no counter round trip (wrong records)
-  r.slot = cx & 7u;
-#else
   r.slot = __hip_atomic_fetch_add(bw.lcnt + r.bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
   return r;
 }
 HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
@@ -1664,9 +1196,6 @@ HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
     r = bw.ovf_base + o;
     if (!ok) __hip_atomic_fetch_or(&g_hn_fault, kFaultBins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#if HN_SC_DIAG >= 1   // diagnostic: no record stores (wrong gradient)
-  ok = ok && v[0] == 1234.5f && v[1] == 5432.1f;
-#endif
   if (ok) {
     *reinterpret_cast<f32x4*>(bw.bins + rec_vofs(r)) = f32x4{v[0], v[1], v[2], v[3]};
     reinterpret_cast<uint32_t*>(bw.bins)[rec_wofs(r, bw.nrec)] = rs.word;
@@ -1697,25 +1226,8 @@ HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], 
 // level; per corner row the x-pair sums over runs of samples in one voxel
 // (16-lane rows, as in the fused scatter) and one record per run head.  Block
 // b is producer b of the record layout (kBwdBlocks blocks).
-#ifndef HN_SC_FASTCELL   // 1: cell from num * RN(1/g) with an exact fallback (voxel_cw_sc)
-#define HN_SC_FASTCELL 1
-#endif
-#ifndef HN_SC_BATCH      // 1: the 4 corner rows' slot round trips before their stores
-#define HN_SC_BATCH 1
-#endif
-#ifndef HN_SC_LANEMAX    // 1: per-level maxima kept per lane in LDS, reduced once per block
-#define HN_SC_LANEMAX 1
-#endif
-#ifndef HN_SC_DIAG       // diagnostics (wrong gradients): 1 no record stores, 2 also no slot counters
-#define HN_SC_DIAG 0
-#endif
-// Coarse-pass feature grads, per ray: 64 samples x 32 features (+ HN_DC_PAD
-// floats, a per-ray stride off the power of two; workspace-internal)
-#ifndef HN_DC_PAD
-#define HN_DC_PAD 0
-#endif
-constexpr size_t kDcRay = (size_t)kSc * 32 + HN_DC_PAD;
-static_assert(HN_DC_PAD % 4 == 0, "f32x4 alignment");
+// Coarse-pass feature grads, per ray: 64 samples x 32 features (workspace-internal)
+constexpr size_t kDcRay = (size_t)kSc * 32;
 // dW(coarse) (+)= sum_b slab[b][0], dW(fine) (+)= sum_b (slab[b][1] +
 // slab[b][2] + slab[b][3]).  64 consecutive elements per block, kSlabGroups
 // slab-groups per element (8 loads in flight per thread, ~18 waves per CU: the
@@ -1729,7 +1241,7 @@ constexpr int kSlabIlp = HN_SLAB_ILP;
 // One slab-reduce block's 64 elements (vblock): the arithmetic of every
 // element is fixed (the group partials, then the pairwise combines), so the
 // sums are the same whichever kernel runs it (slab_reduce_kernel, or the
-// binned scatter's tail, HN_SC_SLAB).  1024 threads; part[16][64] in LDS.
+// binned scatter's tail).  1024 threads; part[16][64] in LDS.
 HN_DEV void slab_reduce_block(const float* __restrict__ slab, int n_blocks, const hn_mlp_grad& dc,
                               const hn_mlp_grad& df, int overwrite, int vblock, float (*part)[64]) {
   const int lane = threadIdx.x & 63;
@@ -1792,36 +1304,20 @@ struct ScK {
   const float* dfeat_c;   // [B][2][1024] tile order (coarse units of the split render_bwd_kernel)
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
-  int32_t scramble;       // render_bwd_kernel's Feistel half-width (HN_SC_PERM), 0: identity
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
   // x-pair of level l (tv_off[L] pairs in all; 0 = no TV term), split evenly
   // over the blocks after their units
   int32_t tv_off[17];
   const float* g_tv;
   TvK tv;
-  // HN_SC_SLAB: the blocks then reduce the MLP backward's dW slabs (the
+  // The blocks then reduce the MLP backward's dW slabs (the
   // slab_reduce_kernel launch folded into this one; same per-element sums)
   const float* slab;       // NULL: no slab reduction here
   hn_mlp_grad dc, df;
   int32_t overwrite_mlp;
 };
-#ifndef HN_SC_SLAB       // 1: the binned scatter's blocks also reduce the dW slabs (no slab_reduce launch)
-#define HN_SC_SLAB 1
-#endif
-__device__ unsigned int g_slab_next;   // next slab block for the scatter blocks (HN_SC_SLAB)
-#ifndef HN_SC_PERM       // 1: a block's rays through the backward's batch permutation
-#define HN_SC_PERM 0
-#endif
-#ifndef HN_SC_ROLL   // 1: levels in a rolled loop of level pairs (one copy of the level code)
-#define HN_SC_ROLL 1
-#endif
+__device__ unsigned int g_slab_next;   // next slab block for the scatter blocks
 constexpr int kScWaves = 16;
-#ifndef HN_SC_LGROUP   // levels per scatter pass (16: all levels per unit at once; 4: level-group major,
-                       // measured slower: scatter 224 -> 264 us, WRITE_SIZE unchanged 613 -> 609 MB)
-#define HN_SC_LGROUP 16
-#endif
-constexpr int kScLG = HN_SC_LGROUP;
-static_assert(kScLG == 4 || kScLG == 8 || kScLG == 16, "level groups of whole tile-order chunks");
 constexpr int kScMaxBinsLog2 = 13;
 constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
 #ifndef HN_BIN_SHIFT_DEFAULT
@@ -1829,7 +1325,7 @@ constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <=
 #endif
 constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per bin (bin_geom)
 
-// HN_SC_STAGE 1: level-major phases across the block's waves (all 16 waves
+// Record staging: level-major phases across the block's waves (all 16 waves
 // take level l of their units, then the block syncs), each head lane's record
 // put into an LDS pool at (bin of the level, slot - the bin's first slot of the
 // phase) and the pool flushed by the block in slot order: a bin's records of
@@ -1843,9 +1339,6 @@ constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per 
 // 1.12x), backward launch time unchanged (0.813 / 0.814 vs 0.813 / 0.812 ms):
 // the scatter waits on its own dependency chains (SQ_WAIT_INST_ANY 44% of its
 // wave cycles), not on the write traffic.
-#ifndef HN_SC_STAGE
-#define HN_SC_STAGE 1
-#endif
 constexpr int kStLog2 = 12, kStPool = 1 << kStLog2;   // 64 KiB of values + 16 KiB of words
 constexpr int kStMinLog2C = 3;                          // fewer than 8 records per bin: no staging
 struct StPhase {
@@ -1865,10 +1358,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __shared__ uint32_t bcnt[kScMaxBins];
   __shared__ float gsl[kGsLds], lvmx[16];
   __shared__ uint32_t lovf;
-#if HN_SC_LANEMAX
   __shared__ uint32_t lvmxl[16 * 64];
   for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) lvmxl[i] = 0u;
-#endif
   const int wave = threadIdx.x >> 6, lane = lane_id();
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
   if (threadIdx.x < 16) lvmx[threadIdx.x] = 0.f;
@@ -1895,8 +1386,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int64_t u0 = (int64_t)blockIdx.x * per;
   const int64_t u1 = u0 + per < units ? u0 + per : units;
   const int pp = lane & 15;
-#if HN_SC_STAGE
-  static_assert(kScLG == 16, "staged phases run all levels of a unit");
   __shared__ f32x4 stv[kStPool];
   __shared__ uint32_t stw[kStPool];
   __shared__ uint32_t stfl[2][kStPool >> kStMinLog2C];   // per phase parity: first staged slot per bin
@@ -1930,48 +1419,18 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   for (int64_t it = 0; it < n_it; ++it) {
     const int64_t u = u0 + wave + it * kScWaves;
     const bool act = u < u1;
-#else
-  // Level groups (HN_SC_LGROUP levels each, level-major over the block's
-  // units): a group's records go to its levels' bins only, so at a time each
-  // producer keeps LG / 16 of its bin regions open -- partially written lines
-  // that would leave L2 before they fill (write amplification) -- and the
-  // group's grads are one tile-order chunk pair (LG = 4: chunk g of both lane
-  // halves), so the loads stay the same; only the ray / point are redone.
-  for (int g = 0; g < 16 / kScLG; ++g)
-  for (int64_t u = u0 + wave; u < u1; u += kScWaves) {
-    constexpr bool act = true;
-#endif
-#if HN_SC_PERM
-    // the block's rays spread over the (spatially ordered) batch: fewer
-    // same-entry records per region at the coarse levels
-    int64_t ray = u / 3;
-    if (k.scramble) {
-      uint32_t x = (uint32_t)ray;
-      do {
-        x = feistel(x, k.scramble, 0x5bd1e995u);
-      } while ((int64_t)x >= k.B);
-      ray = (int64_t)x;
-    }
-#else
     const int64_t ray = u / 3;
-#endif
     const int i = 64 * (int)(u % 3) + lane;       // fine sample
     Ray r;
     float pt[3], xc[3];
     // one level of the unit: voxel, run heads, the 4 corner rows' records
     auto level = [&](const int l, const float g0, const float g1) {
-#if HN_SC_STAGE
         const StPhase ph = st_phase(l, log2T, sh);
         const bool staged = ph.log2c >= kStMinLog2C;
-#endif
         if (act) {
         int32_t cell[3];
         float w[3];
-#if HN_SC_FASTCELL
         voxel_cw_sc(k.g, gsl, pt, xc, l, cell, w);
-#else
-        voxel_cw(k.g, gsl, pt, xc, l, cell, w);
-#endif
         const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
         const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
         const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
@@ -1997,12 +1456,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
           vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
           if (head) rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)k.g.log2T, cx, j ? y0 + kPrimeY : y0,
                                      kk ? z0 + kPrimeZ : z0);
-          if (!HN_SC_BATCH && head) rec_store(bw, rs[c], v[c]);
         }
-        if (HN_SC_BATCH && head) {
+        if (head) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-#if HN_SC_STAGE
             const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[l & 1][staged ? bl : 0];
             if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
               const int q = (int)((bl << ph.log2c) + j);
@@ -2010,32 +1467,20 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
               stw[q] = rs[c].word;
               continue;
             }
-#endif
             rec_store(bw, rs[c], v[c]);
           }
         }
-#if HN_SC_LANEMAX   // per-lane maxima in LDS (one conflict-free ds_max per level), reduced once per block
         __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-        vmax = wave_max_f32(vmax);
-        if (lane == 0)
-          __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), __float_as_uint(vmax), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
         }   // act
-#if HN_SC_STAGE
       __syncthreads();   // the phase's records are in the pool, its counts final
       st_flush(l);
       st_init(l + 1 < 16 ? l + 1 : 0);   // the next phase's bins (other parity), counts unchanged by the flush
       __syncthreads();   // the pool is free again
-#endif
     };
-#if HN_SC_ROLL
     // grads loaded per level pair inside a rolled loop (one copy of the level
     // code for two levels instead of sixteen: the unrolled kernel was 84 KB,
     // over the 64 KB instruction cache two CUs share)
-    static_assert(kScLG == 16, "rolled levels: all levels of a unit");
     const f32x4* tb = nullptr;
     const f32x4* tw = nullptr;
     int src = kSc;
@@ -2069,57 +1514,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     // non-finite inputs (NaN / Inf in a grad or the point): one test per lane
     if (act && __ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
       __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    float gf[2][kScLG];
-    if (act) {
-    load_ray(k.rays, ray, r);
-    ray_point(r, k.z_fine[ray * kSf + i], pt);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
-    // grads [f][level - LG g]: tile-order chunks c of lanes (p, h = 0) and (p, h = 1)
-    // (levels 4c .. 4c + 3 live in chunk c: tile_level)
-    constexpr int NC = kScLG / 4;
-    const f32x4* tb = reinterpret_cast<const f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int cc = 0; cc < NC; ++cc) {
-        const f32x4 q = tb[64 * (NC * g + cc) + 32 * h + (i & 31)];
-        const float e[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int reg = 4 * cc + j;   // relative to the group's first chunk
-          gf[reg & 1][tile_level(reg >> 1, h)] = e[j];
-        }
-      }
-    const int src = k.fine_src[ray * kSf + i];
-    if (src < kSc) {                              // coarse twin: fine + coarse grads
-      const f32x4* tw = reinterpret_cast<const f32x4*>(k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-          const f32x4 q = tw[64 * (NC * g + cc) + 32 * h + (src & 31)];
-          const float e[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int reg = 4 * cc + j;
-            float& d = gf[reg & 1][tile_level(reg >> 1, h)];
-            d = d + e[j];
-          }
-        }
-    }
-    {   // non-finite inputs (NaN / Inf in a grad or the point): one sum, one test per lane
-      float chk = (pt[0] + pt[1]) + pt[2];
-#pragma unroll
-      for (int ll = 0; ll < kScLG; ++ll) chk += gf[0][ll] + gf[1][ll];
-      if (__ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
-        __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    }   // act
-#pragma unroll
-    for (int ll = 0; ll < kScLG; ++ll) level(kScLG * g + ll, gf[0][ll], gf[1][ll]);
-#endif
   }
   if (k.tv_off[16] > 0) {
     // The TV term's table gradient: one record per x-pair (x0, x0 + 1) of cube
@@ -2154,7 +1548,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     }
   }
   __syncthreads();
-#if HN_SC_LANEMAX
   if (wave == 0) {   // lane = level: the max of its 64 lane slots
     const int l = lane & 15, q = lane >> 4;
     uint32_t m = 0u;
@@ -2162,7 +1555,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&lvmx[l]), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
-#endif
   uint32_t* cnt = book + nrec + blockIdx.x;
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
     const uint32_t c = bcnt[i];
@@ -2199,7 +1591,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 // The table-gradient scatter of one slot (embedding_dense_backward of
 // hash_encoding.py:106 + trilinear backward); V = 2048-float voxel buffer.
 template <int CAP>
-HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl, AQ& aq) {
+HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gsl) {
   const int lane = lane_id();
   const int pp = lane & 15, f = (lane >> 4) & 1, lq = lane >> 4;
   Ray r;
@@ -2208,7 +1600,6 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
     r.o[a] = S[kSlotR + a];
     r.d[a] = S[kSlotR + 3 + a];
   }
-  [[maybe_unused]] uint32_t cont = 0u;
 #pragma unroll
   for (int grp = 0; grp < 2; ++grp) {
     float pt[3], xc[3];
@@ -2229,35 +1620,7 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
                                               __uint_as_float((uint32_t)cell[2] * kPrimeZ), w[0]};
       *reinterpret_cast<float2*>(dst + 4) = make_float2(w[1], w[2]);
     }
-#if HN_TILE_RUNS
-    float* const cc = V + 16 * 16 * 8;          // [level][cx, cy*PY, cz*PZ, -]: group 1's first point
-    if (grp == 0 && lane < 16) {                // lane = level
-      float p16[3], x16[3];
-      ray_point(r, S[kSlotZ + 16], p16);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) x16[a] = clamp_t(p16[a], k.g.bmin[a], k.g.bmax[a]);
-      int32_t cell[3];
-      float w[3];
-      voxel_cw(k.g, gsl, p16, x16, lane, cell, w);
-      *reinterpret_cast<f32x4*>(cc + 4 * lane) =
-          f32x4{__int_as_float(cell[0]), __uint_as_float((uint32_t)cell[1] * kPrimeY),
-                __uint_as_float((uint32_t)cell[2] * kPrimeZ), 0.f};
-    }
-#endif
     lds_fence_wave();
-#if HN_TILE_RUNS
-    if (grp == 0) {                             // bit l: group 0's last cell at level l == group 1's first
-      const int li = lane & 15;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(V + (li * 16 + 15) * 8);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(cc + 4 * li);
-      const bool eq = __float_as_uint(a.x) == __float_as_uint(b.x) && __float_as_uint(a.y) == __float_as_uint(b.y) &&
-                      __float_as_uint(a.z) == __float_as_uint(b.z);
-      cont = (uint32_t)__ballot(eq) & 0xffffu;
-#ifdef HN_TILE_RUNS_OFF   // diagnostic: the carry's overhead without its merges
-      cont = 0u;
-#endif
-    }
-#endif
     float gl[16];
     const f32x4* src4 = reinterpret_cast<const f32x4*>(S + (16 * grp + pp) * kXS + 16 * f);
 #pragma unroll
@@ -2270,32 +1633,15 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
     const float* vs = V + pp * 8;
     f32x4 v0 = *reinterpret_cast<const f32x4*>(vs);
     float2 v1 = *reinterpret_cast<const float2*>(vs + 4);
-#if HN_TILE_RUNS
-    // held sums [level][lane-in-unit][row], read one level ahead like the records
-    float* const cs = V + 16 * 16 * 8 + 64 + 4 * (lane >> 4);
-    f32x4 cr = grp ? *reinterpret_cast<const f32x4*>(cs) : f32x4{};
-#endif
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
       const f32x4 c0 = v0;
       const float2 c1 = v1;
-#if HN_TILE_RUNS
-      const f32x4 cc0 = cr;
-#endif
       if (l < 15) {
         v0 = *reinterpret_cast<const f32x4*>(vs + (l + 1) * 128);
         v1 = *reinterpret_cast<const float2*>(vs + (l + 1) * 128 + 4);
-#if HN_TILE_RUNS
-        if (grp) cr = *reinterpret_cast<const f32x4*>(cs + 16 * (l + 1));
-#endif
       }
-#if HN_TILE_RUNS
-      const bool cl = (cont >> l) & 1u;
-      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq, cl && grp == 0, cl && grp == 1, cc0,
-                           cs + 16 * l);
-#else
-      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane, aq);
-#endif
+      scatter_level_x<CAP>(k.g, k.d_table, c0, c1, l, gl[l], lane);
       if ((l & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -2305,13 +1651,7 @@ HN_DEV void scatter_slot(const B1K& k, const float* S, float* V, const float* gs
 // Producer: one fine tile.  A fine sample that is one of the 64 coarse
 // samples (fine_src < 64) is the same point in both passes: its coarse-pass
 // grads are added, so every unique point is scattered once.  z / src: this
-// lane's point's depth and fine_src (prefetched per unit).  When the ring is
-// full (the scatter wave is behind), the MLP wave scatters the tile itself in
-// its own image region X (free between tiles) instead of waiting; its next
-// global load then waits for those atomics once.
-#ifndef HN_MW_SELF
-#define HN_MW_SELF 0
-#endif
+// lane's point's depth and fine_src (prefetched per unit).
 HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_t ray, float z, int src,
                      const f32x16& dfeat) {
   const int lane = lane_id();
@@ -2322,17 +1662,6 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
   f32x4 tw[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) tw[c] = twin ? dc[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-  if (HN_MW_SELF) {
-    const int tn = lds_load(q.tick);
-    if (lds_load(&q.freed[tn % kSlots]) < tn / kSlots) {   // next slot still occupied
-      if (lane == 0) atomicAdd(q.selfc, 1);
-      fill_slot(X, r, z, dfeat, tw);
-      static_assert(!HN_MW_SELF || !HN_COMPACT, "the compacted queue belongs to the scatter wave");
-      AQ none{nullptr, 0u, 0u, 0u, {}, 0ull};
-      scatter_slot<HN_SW_VMCNT>(k, X, X + kSlotF, q.gsl, none);
-      return;
-    }
-  }
   int t = 0;
   if (lane == 0) t = atomicAdd(q.tick, 1);
   t = __builtin_amdgcn_readfirstlane(t);
@@ -2344,17 +1673,13 @@ HN_DEV void ring_put(const B1K& k, const Ring& q, float* X, const Ray& r, int64_
 }
 
 // Consumer: takes tickets in order until every one of the n_tiles fine tiles
-// is accounted for (a ticket, or scattered by its MLP wave).  tick and selfc
-// only grow and a tile is counted before it is handled, so tick + selfc ==
-// n_tiles with t >= tick means no ticket t will ever come.
+// has a ticket.  tick only grows and a tile takes its ticket before it is
+// handed over, so tick == n_tiles with t >= tick means no ticket t will ever
+// come.
 template <int CAP>
 HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
-  AQ aq{reinterpret_cast<float2*>(V + kVoxF), 0u, 0u, 0u, {}, 0ull};
   for (int t = 0;; ++t) {
     const int s = t % kSlots;
-#if HN_PROFILE
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-#endif
     bool have = false, done = false;
     for (int it = 0; it < kSpinCap; ++it) {
       if (lds_load(&q.ready[s]) >= t + 1) {
@@ -2362,7 +1687,7 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
         break;
       }
       const int tk = lds_load(q.tick);
-      if (tk + lds_load(q.selfc) >= n_tiles && t >= tk) {
+      if (tk >= n_tiles && t >= tk) {
         done = true;
         break;
       }
@@ -2370,18 +1695,11 @@ HN_DEV void ring_drain(const B1K& k, const Ring& q, float* V, int n_tiles) {
     }
     if (!have && !done) raise_fault(kFaultDrain);   // tiles left unscattered
     asm volatile("" ::: "memory");
-#if HN_PROFILE
-    if (lane_id() == 0) atomicAdd(&g_ring[1], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
-#endif
     if (!have) break;
     const float* S = q.slots + s * kSlotF;
-    scatter_slot<CAP>(k, S, V, q.gsl, aq);
+    scatter_slot<CAP>(k, S, V, q.gsl);
     ring_publish(&q.freed[s], t / kSlots + 1);
   }
-  if (HN_COMPACT) aq_drain(k.d_table, aq, lane_id());
-#if HN_PROFILE
-  if (lane_id() == 0) atomicAdd(&g_ring[4], (unsigned long long)aq.cap_wait);
-#endif
 }
 
 HN_DEV void wait_flag(int* flag, int need) {
@@ -2396,38 +1714,14 @@ HN_DEV void wait_flag(int* flag, int need) {
 // Fine units hand each tile to the scatter wave; before the first hand-off
 // they wait until wave 0 has published this ray's coarse feature grads
 // (*done >= need)
-// Split schedule: a wave's units are known in advance (static split), so the
-// next unit's first inputs -- its first tile's saved features and its ray's
-// view direction -- are loaded while the current unit's second tile runs,
-// instead of exposing their HBM latency at every unit start (HN_B1_PREFETCH).
-#ifndef HN_B1_PREFETCH
-#define HN_B1_PREFETCH 0
-#endif
-struct UnitPre {
-  f32x16 feat;      // this unit's first-tile features (loaded by the previous unit)
-  float vd[3];      // this unit's view direction
-  int64_t next;     // the next unit's ray, or -1
-};
-HN_DEV void unit_pre_load(const B1K& k, int64_t ray, int ctile, int lane, UnitPre& u) {
-  load_feat(k.feat, ray, ctile, lane, u.feat);
-#pragma unroll
-  for (int a = 0; a < 3; ++a) u.vd[a] = k.rays[11 * ray + 8 + a];
-}
-
 template <int S, int MODE>
 HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing& wr, const Ring* ring,
-                    PhaseClock& pc, int* done = nullptr, int need = 0, UnitPre* pre = nullptr) {
-  pc.start();
+                    int* done = nullptr, int need = 0) {
   const int lane = lane_id();
   constexpr bool fine = S == kSf;
   const int p = lane & 31, h = lane >> 5;
   Ray r;
-  if (pre != nullptr) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) r.vd[a] = pre->vd[a];   // the split backward needs only the view direction
-  } else {
-    load_ray(k.rays, ray, r);
-  }
+  load_ray(k.rays, ray, r);
   const int tile0 = 2 * part;                   // tile within this pass
   const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
   float4 dr[2];
@@ -2448,7 +1742,6 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   // color_net.0 applied to the sh part: the same for every point of the ray
   // (and bit-identical to starting each point's chain with it)
   C0Sh c0sh;
-#if HN_C0SH_LDS
   {
     float* cl = X + kC0shF;
 #pragma unroll
@@ -2463,11 +1756,6 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
     lds_fence_wave();
     c0sh.lds = cl;
   }
-#else
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob)
-    c0sh.v[ob] = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
-#endif
   const int ctile = (fine ? kSc / 32 : 0) + tile0;
   float zq[2] = {0.f, 0.f};
   int srcq[2] = {0, 0};
@@ -2479,27 +1767,13 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
     }
   }
   f32x16 feat, featn;
-  if (pre != nullptr)
-    feat = pre->feat;
-  else
-    load_feat(k.feat, ray, ctile, lane, feat);
+  load_feat(k.feat, ray, ctile, lane, feat);
   load_feat(k.feat, ray, ctile + 1, lane, featn);
   static_for<0, 2>([&](auto tc) {   // unrolled: the ring's slots and the per-tile arrays stay static
     constexpr int t = decltype(tc)::value;
-    if (t == 0) HN_LAP(pc, unit);
-#if HN_ABLATE == 2   // diagnostic build: no MLP backward, the scatter runs on stand-in grads
-    f32x16 dfeat = t ? featn : feat;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dfeat[r] *= dr[t].x;
-#else
     uint32_t sm[3] = {0u, 0u, 0u};
-    if (HN_B1_SMASK) load_masks(k.feat, ray, ctile + t, lane, sm);
-    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw, sm, [&]() {
-      if (t == 1 && pre != nullptr && pre->next >= 0)   // the next unit's first inputs, during tile 1
-        unit_pre_load(k, pre->next, ctile, lane, *pre);
-    });
-#endif
-    HN_LAP(pc, mlp);
+    load_masks(k.feat, ray, ctile + t, lane, sm);
+    const f32x16 dfeat = b1_tile(P, wr, X, t ? featn : feat, c0sh, dr[t], dw, sm);
     const int qbase = 32 * (tile0 + t);
     if constexpr (fine && MODE == kModeSplit) {
       // split backward: the tile's feature grads in the saved-feature tile
@@ -2508,21 +1782,9 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
       f32x4* dst = reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + tile0 + t) * 1024);
 #pragma unroll
       for (int c = 0; c < 4; ++c) dst[64 * c + lane] = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
-      HN_LAP(pc, scat);
     } else if constexpr (fine) {
-#if HN_PROFILE
-      const uint64_t tw0 = __builtin_amdgcn_s_memtime();
-#endif
       if (t == 0) wait_flag(done, need);       // the coarse twin grads are written
-#if HN_PROFILE
-      if (lane == 0) atomicAdd(&g_ring[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
-#endif
-#if HN_ABLATE == 3   // diagnostic build: MLP backward only, the fine tiles' feature grads are dropped
-      if (dfeat[0] == 1234.5f && dfeat[1] == -1234.5f) X[lane] = dfeat[2] + zq[t] + (float)srcq[t];
-#else
       ring_put(k, *ring, X, r, ray, zq[t], srcq[t], dfeat);
-#endif
-      HN_LAP(pc, scat);
     } else if constexpr (MODE == kModeSplit) {
       // coarse, split backward: the tile's feature grads in the saved-feature
       // tile order like the fine tiles (4 coalesced dwordx4 stores; the
@@ -2544,28 +1806,18 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
   });
 }
 
-// HN_B1_ONECOPY 1 (split backward): the coarse and fine units share one code
+// Split backward: the coarse and fine units share one code
 // path (the pass is a runtime flag: weights, draw offset, tile index and
 // destination are selects) and the unit's two tiles run as a loop, so the
 // kernel holds ONE copy of b1_tile instead of four (two unrolled tiles x two
 // unit templates): 87 KB of code -> ~25 KB, under the 64 KB instruction cache
 // two CUs share (wave 0 ran the coarse copies, waves 1-3 the fine ones, at
 // the same time).
-#ifndef HN_B1_ONECOPY
-#define HN_B1_ONECOPY 1
-#endif
-HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float* X, DW& dw, WRing& wr,
-                          PhaseClock& pc, UnitPre* pre) {
-  pc.start();
+HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float* X, DW& dw, WRing& wr) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
   Ray r;
-  if (pre != nullptr) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) r.vd[a] = pre->vd[a];
-  } else {
-    load_ray(k.rays, ray, r);
-  }
+  load_ray(k.rays, ray, r);
   const int tile0 = 2 * part;
   const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
   float4 dr[2];
@@ -2584,7 +1836,6 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
   }
   const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
   C0Sh c0sh;
-#if HN_C0SH_LDS
   {
     float* cl = X + kC0shF;
 #pragma unroll
@@ -2599,37 +1850,23 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
     lds_fence_wave();
     c0sh.lds = cl;
   }
-#else
-#pragma unroll
-  for (int ob = 0; ob < 2; ++ob)
-    c0sh.v[ob] = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
-#endif
   const int ctile = (fine ? kSc / 32 : 0) + tile0;
   f32x16 feat, featn;
-  if (pre != nullptr)
-    feat = pre->feat;
-  else
-    load_feat(k.feat, ray, ctile, lane, feat);
+  load_feat(k.feat, ray, ctile, lane, feat);
   load_feat(k.feat, ray, ctile + 1, lane, featn);
   // this unit's feature-grad tiles (the saved-feature tile order of both passes)
   f32x4* dst0 = fine ? reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + tile0) * 1024)
                      : reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)tile0 * 1024);
-  HN_LAP(pc, unit);
 #pragma clang loop unroll(disable)
   for (int t = 0; t < 2; ++t) {
     const float4 drt = t ? dr[1] : dr[0];
     uint32_t sm[3] = {0u, 0u, 0u};
-    if (HN_B1_SMASK) load_masks(k.feat, ray, ctile + t, lane, sm);
-    const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, drt, dw, sm, [&]() {
-      if (t == 1 && pre != nullptr && pre->next >= 0)   // the next unit's first inputs, during tile 1
-        unit_pre_load(k, pre->next, (fine ? kSc / 32 : 0) + tile0, lane, *pre);
-    });
-    HN_LAP(pc, mlp);
+    load_masks(k.feat, ray, ctile + t, lane, sm);
+    const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, drt, dw, sm);
     f32x4* dst = dst0 + 256 * t;
 #pragma unroll
     for (int c = 0; c < 4; ++c) dst[64 * c + lane] = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
     feat = featn;
-    HN_LAP(pc, scat);
   }
 }
 
@@ -2772,21 +2009,21 @@ void render_bwd_kernel(B1K k) {
   float* X = smem + wave * kRRows * kXS;
   float* slots = smem + kB1Img;
   float* V = slots + kSlots * kSlotF;
-  float* gsl = V + kVoxF + 2 * kQ;               // [voxel buffer | atomic queue | grid sizes | sync]
+  float* gsl = V + kVoxF;                        // [voxel buffer | grid sizes | sync]
   // [0] coarse rays done, [1] fine units taken, [2] ring tickets, [3] dW buffer zeroed,
-  // [4] self-scattered tiles, [5..) ready, freed
+  // [4] unused, [5..) ready, freed
   int* sync = reinterpret_cast<int*>(gsl + kGsLds);
   stage_grid_sizes(k.g, gsl);
   if (threadIdx.x < kSyncInts) sync[threadIdx.x] = 0;
   __syncthreads();
-  const Ring ring{slots, &sync[2], &sync[4], &sync[5], &sync[5 + kSlots], gsl};
+  const Ring ring{slots, &sync[2], &sync[5], &sync[5 + kSlots], gsl};
   const int64_t nb = gridDim.x;
   const int n_rays = k.B > (int64_t)blockIdx.x ? (int)((k.B - 1 - blockIdx.x) / nb + 1) : 0;
   // ray of the block's i-th unit: a contiguous chunk per block when the
   // batch divides evenly, so the rays in flight at one time across the chip
   // are far apart in a spatially ordered batch (concurrent atomics on the
   // same rows serialize at the memory side); strided otherwise
-  const bool chunked = HN_BWD_CHUNK && k.B % nb == 0;
+  const bool chunked = k.B % nb == 0;
   auto block_ray = [&](int64_t i) -> int64_t {
     if (!chunked) return (int64_t)blockIdx.x + i * nb;
     // a fixed pseudo-random permutation of the batch scatters both the rays in
@@ -2802,41 +2039,24 @@ void render_bwd_kernel(B1K k) {
   DW dw;
   dw_zero(dw);
   WRing wr;
-  PhaseClock pc;
-#if HN_PROFILE
-  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
-#endif
   if (wave == kMW && !SPLIT) {
-    ring_drain<CAP>(k, ring, V, HN_ABLATE == 3 ? 0 : 2 * kSf / 64 * n_rays);
-#if HN_PROFILE
-    if (lane == 0) atomicAdd(&g_ring[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
-#endif
-  } else if (SPLIT && HN_B1_ONECOPY) {
+    ring_drain<CAP>(k, ring, V, 2 * kSf / 64 * n_rays);
+  } else if (SPLIT) {
     // split: wave 0 the block's coarse units (slab slot 0), waves 1-3 part
     // wave - 1 of every ray's fine units (slots 1-3) -- a static split, so each
     // dW slab, and with the fixed-order slab reduce the MLP gradients, are
     // bitwise reproducible
-    UnitPre pre;
-    UnitPre* prep = HN_B1_PREFETCH ? &pre : nullptr;
     const int wv = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform (SGPR) pass and part
     const bool fine = wv != 0;
     const int part = fine ? wv - 1 : 0;
     wring_prime(wr, fine ? k.Pf : k.Pc, lane);
-    if (prep && n_rays > 0) unit_pre_load(k, block_ray(0), (fine ? kSc / 32 : 0) + 2 * part, lane, pre);
-    for (int i = 0; i < n_rays; ++i) {
-      pre.next = i + 1 < n_rays ? block_ray(i + 1) : -1;
-      b1_unit_split(k, block_ray(i), part, fine, X, dw, wr, pc, prep);
-    }
+    for (int i = 0; i < n_rays; ++i) b1_unit_split(k, block_ray(i), part, fine, X, dw, wr);
     dw_flush<true>(dw, k.slab + ((size_t)blockIdx.x * kSlabSlots + wv) * W_END, lane);
   } else {
-    UnitPre pre;
-    UnitPre* prep = SPLIT && HN_B1_PREFETCH ? &pre : nullptr;
     if (wave == 0) {
       wring_prime(wr, k.Pc, lane);
-      if (prep && n_rays > 0) unit_pre_load(k, block_ray(0), 0, lane, pre);
       for (int i = 0; i < n_rays; ++i) {
-        pre.next = i + 1 < n_rays ? block_ray(i + 1) : -1;
-        b1_unit<kSc, MODE>(k, block_ray(i), 0, X, dw, wr, nullptr, pc, nullptr, 0, prep);
+        b1_unit<kSc, MODE>(k, block_ray(i), 0, X, dw, wr, nullptr);
         if constexpr (!SPLIT) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this ray's feature grads are in L2
           if (lane == 0) __hip_atomic_store(&sync[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2853,11 +2073,7 @@ void render_bwd_kernel(B1K k) {
       // dW slab, and with the fixed-order slab reduce the MLP gradients, are
       // bitwise reproducible
       wring_prime(wr, k.Pf, lane);
-      if (prep && n_rays > 0) unit_pre_load(k, block_ray(0), kSc / 32 + 2 * (wave - 1), lane, pre);
-      for (int i = 0; i < n_rays; ++i) {
-        pre.next = i + 1 < n_rays ? block_ray(i + 1) : -1;
-        b1_unit<kSf, MODE>(k, block_ray(i), wave - 1, X, dw, wr, &ring, pc, &sync[0], i + 1, prep);
-      }
+      for (int i = 0; i < n_rays; ++i) b1_unit<kSf, MODE>(k, block_ray(i), wave - 1, X, dw, wr, &ring, &sync[0], i + 1);
     } else if (!SPLIT) {
       wring_prime(wr, k.Pf, lane);
       for (;;) {
@@ -2865,7 +2081,7 @@ void render_bwd_kernel(B1K k) {
         if (lane == 0) u = atomicAdd(&sync[1], 1);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= 3 * n_rays) break;
-        b1_unit<kSf, MODE>(k, block_ray(u / 3), u % 3, X, dw, wr, &ring, pc, &sync[0], u / 3 + 1);
+        b1_unit<kSf, MODE>(k, block_ray(u / 3), u % 3, X, dw, wr, &ring, &sync[0], u / 3 + 1);
       }
     }
     // every fine MLP wave stores its fine dW to its own slab slot (split:
@@ -2877,16 +2093,6 @@ void render_bwd_kernel(B1K k) {
     if (!SPLIT || wave != 0)
       dw_flush<true>(dw, k.slab + ((size_t)blockIdx.x * kSlabSlots + (SPLIT ? wave : wave + 1)) * W_END, lane);
   }
-#if HN_PROFILE
-  if (lane == 0 && wave < kMW) {
-    const int role = wave == 0 ? 0 : 1;
-    atomicAdd(&g_phase[role][0], (unsigned long long)pc.unit);
-    atomicAdd(&g_phase[role][1], (unsigned long long)pc.mlp);
-    atomicAdd(&g_phase[role][2], (unsigned long long)pc.scat);
-    atomicAdd(&g_phase[role][3], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
-    atomicAdd(&g_phase[role][4], 1ull);
-  }
-#endif
 }
 
 __global__ __launch_bounds__(64 * kSlabGroups) void slab_reduce_kernel(const float* __restrict__ slab, int n_blocks,
@@ -2935,24 +2141,12 @@ constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2
 // after the setup 238 us, after the thread's last record fetch 217 us (64
 // VGPR spills): vmcnt waits are in order, so an earlier issue only moves the
 // wait to the first records.
-#ifndef HN_BR_PF
-#define HN_BR_PF 0
-#endif
-#ifndef HN_BR_REV
-#define HN_BR_REV 0
-#endif
 static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
 #ifndef HN_BR_DEPTH   // records per thread and fetch group (two groups in flight)
 #define HN_BR_DEPTH 4
 #endif
 constexpr int kBrDepth = HN_BR_DEPTH;
-#ifndef HN_BR_SEARCH   // 1: a record's region from a per-64-record-chunk table + a forward walk
-#define HN_BR_SEARCH 1
-#endif
 constexpr int kBrChunks = 8192;   // table entries (16 KiB of LDS): bins of up to 512 K records
-#ifndef HN_BR_DIAG   // diagnostic: 1 record loads only (wrong gradient)
-#define HN_BR_DIAG 0
-#endif
 
 // round(v * 2^S) as int64 without f64 arithmetic: x = v * 2^S is exact in fp32
 // (|x| < 2^41, a power-of-2 scale), a = trunc(x / 2^16) is an exact integer,
@@ -2969,18 +2163,9 @@ HN_DEV long long fx_of(float v, float scale) {
 // wave's random entries spread over twice the LDS banks of [entry][feature])
 HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_t w, uint32_t sel,
                     uint32_t tmask, float scale) {
-#if HN_BR_DIAG == 2   // diagnostic: entries scrambled per lane (no same-address serialisation; wrong gradient)
-  const uint32_t e0 = ((w & 0x0fffffffu) ^ (__lane_id() * 97u)) & sel;
-#else
   const uint32_t e0 = w & 0x0fffffffu & sel;
-#endif
   const uint32_t e1 = e0 ^ (((1u << (w >> 28)) - 1u) & tmask);
-#if HN_BR_DIAG == 3   // diagnostic: no fixed-point conversion (wrong gradient)
-  const long long q[4] = {(long long)__float_as_int(v.x), (long long)__float_as_int(v.y),
-                          (long long)__float_as_int(v.z), (long long)__float_as_int(v.w)};
-#else
   const long long q[4] = {fx_of(v.x, scale), fx_of(v.y, scale), fx_of(v.z, scale), fx_of(v.w, scale)};
-#endif
   __hip_atomic_fetch_add(acc + e0, (unsigned long long)q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_add(acc + se + e0, (unsigned long long)q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_add(acc + e1, (unsigned long long)q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3053,33 +2238,15 @@ __global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
 // records i, i + 1024, ... (4 at a time, independent loads in flight) and
 // finds each one's region by binary search over the LDS prefix of the
 // regions' counts.
-#ifndef HN_BR_PROF   // diagnostic: phase timers of the owner pass (scripts/br_profile.sh)
-#define HN_BR_PROF 0
-#endif
-#if HN_BR_PROF
-__device__ unsigned long long g_brprof[8];
-#define HN_BR_T(i) do { __syncthreads(); if (threadIdx.x == 0) { const uint64_t n_ = __builtin_amdgcn_s_memtime(); \
-    atomicAdd(&g_brprof[i], (unsigned long long)(n_ - t_br)); t_br = n_; } } while (0)
-#else
-#define HN_BR_T(i) ((void)0)
-#endif
 __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
-#if HN_BR_PROF
-  uint64_t t_br = __builtin_amdgcn_s_memtime();
-#endif
   extern __shared__ f32x4 acc4[];
   __shared__ uint32_t pre[kBwdBlocks + 1];
   __shared__ uint32_t wsum[kBwdBlocks / 64], wmax[kBwdBlocks / 64];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(acc4);
   const int n4 = (2 << k.shift) / 2;   // f32x4 = 2 accumulators
-#if HN_BR_REV   // the finest levels' (heaviest) bins dispatched first, the light coarse ones fill the tail
-  const uint32_t b = gridDim.x - 1u - blockIdx.x;
-#else
   const uint32_t b = blockIdx.x;
-#endif
   const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
   const int nd4 = (2 << k.shift) / 4;             // float4s of the slice (<= 4 per thread)
-  float4 sp[kSliceF4], sm[kSliceF4], sv[kSliceF4];
   // fused step on a coarse level: the row pairs no gradient can reach (their
   // moments are zero, so the dense update leaves p, m, v bitwise unchanged)
   // are neither loaded nor stored (table_live; T=19: levels 0-6)
@@ -3087,18 +2254,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   if (k.fused && k.live && k.shift <= k.log2T && (int)(((uint32_t)b << k.shift) >> k.log2T) < k.live_levels)
     lw = k.live + (((size_t)b << k.shift) >> 6);
   auto live_at = [&](int i) { return lw == nullptr || ((lw[i >> 5] >> (i & 31)) & 1u) != 0u; };
-  auto load_state = [&]() {
-#pragma unroll
-    for (int j = 0; j < kSliceF4; ++j) {
-      const int i = threadIdx.x + j * kBinThreads;
-      if (i < nd4 && live_at(i)) {
-        sp[j] = reinterpret_cast<const float4*>(k.step.p + e0)[i];
-        sm[j] = reinterpret_cast<const float4*>(k.step.m + e0)[i];
-        sv[j] = reinterpret_cast<const float4*>(k.step.v + e0)[i];
-      }
-    }
-  };
-  if (HN_BR_PF == 1 && k.fused) load_state();
   for (int i = threadIdx.x; i < n4; i += kBinThreads) acc4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
   const uint32_t* words = reinterpret_cast<const uint32_t*>(k.bins);
@@ -3142,7 +2297,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __syncthreads();
   const uint32_t total = pre[kBwdBlocks];
   const uint32_t sel = (1u << k.shift) - 1u, tmask = (1u << k.log2T) - 1u, se = 1u << k.shift;
-#if HN_BR_SEARCH
   // region of the first record of every 64-record chunk: a record's region is
   // then a short forward walk from its chunk's (regions hold ~24-114 records)
   // instead of an 8-step binary search
@@ -3159,12 +2313,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     }
     __syncthreads();
   }
-#endif
-  HN_BR_T(0);   // accumulator zeroing, counts, prefix, scale
   const size_t bbase = (size_t)b * kBwdBlocks * k.cap;
   // records r0 + q * 1024 (lane-consecutive: coalesced loads), each found in
-  // the regions' prefix from its 64-record chunk's first region (HN_BR_SEARCH;
-  // else a binary search; both measured faster than one search per 4
+  // the regions' prefix from its 64-record chunk's first region (a binary
+  // search per record measured slower; both faster than one search per 4
   // lane-consecutive records with their 64-B-strided loads); the next group
   // of records is loaded before the current one is added
   auto fetch = [&](uint32_t r0, f32x4 (&v)[kBrDepth], uint32_t (&w)[kBrDepth]) {
@@ -3173,12 +2325,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       const uint32_t r = r0 + q * kBinThreads;
       if (r < total) {
         int lo = 0;   // largest p with pre[p] <= r
-#if HN_BR_SEARCH
         if (tab) {
           lo = first_reg[r >> 6];
           while (pre[lo + 1] <= r) ++lo;   // r < total = pre[kBwdBlocks]: stops by lo = 255
         } else
-#endif
         {
 #pragma unroll
           for (int st = kBwdBlocks / 2; st >= 1; st >>= 1)
@@ -3194,11 +2344,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
 #pragma unroll
     for (int q = 0; q < kBrDepth; ++q)
       if (r0 + q * kBinThreads < total) {
-#if HN_BR_DIAG == 1   // diagnostic: record loads only
-        if (v[q].x == 1234.5f && w[q] == 7u) acc[threadIdx.x] = 1ull;
-#else
         bin_add(acc, se, v[q], w[q], sel, tmask, scale);
-#endif
       }
   };
   f32x4 va[kBrDepth], vb[kBrDepth];
@@ -3213,7 +2359,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     if (r1 + kBrDepth * kBinThreads < total) fetch(r1 + kBrDepth * kBinThreads, va, wa);
     add(r1, vb, wb);
   }
-  HN_BR_T(1);   // region records
   if (n_ovf) {   // this bin's spilled records (bucketed by ovf_place_kernel)
     const size_t ob = (size_t)kBwdBlocks * k.nbins * k.cap;
     const uint32_t lo = obk.first[b], hi = lo + obk.per_bin[b];
@@ -3224,7 +2369,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
     }
   }
   __syncthreads();
-  HN_BR_T(2);   // overflow records
   const double inv = 1.0 / (double)scale;
   float4* dst = k.d_table ? reinterpret_cast<float4*>(k.d_table + e0) : nullptr;
 #pragma unroll
@@ -3247,12 +2391,9 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       if (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f)
         __hip_atomic_fetch_or(&g_hn_fault, kFaultDeadRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (k.fused) {   // RAdam on these 4 table elements (radam_kernel's update, same op forms)
-      if (HN_BR_PF == 0) {
-        sp[j] = reinterpret_cast<const float4*>(k.step.p + e0)[i];
-        sm[j] = reinterpret_cast<const float4*>(k.step.m + e0)[i];
-        sv[j] = reinterpret_cast<const float4*>(k.step.v + e0)[i];
-      }
-      float4 p = sp[j], m = sm[j], v = sv[j];
+      float4 p = reinterpret_cast<const float4*>(k.step.p + e0)[i];
+      float4 m = reinterpret_cast<const float4*>(k.step.m + e0)[i];
+      float4 v = reinterpret_cast<const float4*>(k.step.v + e0)[i];
       radam_elem(k.step, p.x, a.x, m.x, v.x);
       radam_elem(k.step, p.y, a.y, m.y, v.y);
       radam_elem(k.step, p.z, a.z, m.z, v.z);
@@ -3262,7 +2403,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
       if (k.step.mode != 0) reinterpret_cast<float4*>(k.step.p + e0)[i] = p;
     }
   }
-  HN_BR_T(3);   // conversion, RAdam, stores issued
 }
 
 static int32_t check_cfg(const hn_render_cfg* c) {
@@ -3429,19 +2569,6 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdWaves - 1) / kFwdWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdWaves), 0, s, k);
-#if HN_PROFILE
-  {
-    unsigned long long f[8];
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_fwd), sizeof(f));
-    const double w = f[7] ? (double)f[7] : 1.;
-    fprintf(stderr, "hn_fwd_profile cycles/wave: coarse encode %.0f mlp %.0f | sample %.0f | fine encode %.0f "
-            "mlp %.0f | composite %.0f | total %.0f\n", f[0] / w, f[1] / w, f[2] / w, f[3] / w, f[4] / w,
-            f[5] / w, f[6] / w);
-    memset(f, 0, sizeof(f));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd), f, sizeof(f));
-  }
-#endif
   return hip_status(hipGetLastError());
 }
 
@@ -3469,7 +2596,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   B1K k;
   k.B = a->n_rays;
   k.scramble = 0;
-  if (HN_BWD_SCRAMBLE && a->n_rays > 1) {
+  if (a->n_rays > 1) {
     int bits = 2;
     while ((1ll << bits) < a->n_rays) bits += 2;
     k.scramble = bits / 2;
@@ -3554,7 +2681,6 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.bin_cap = k.bin_cap;
     sk.bin_shift = k.bin_shift;
     sk.nbins = k.nbins;
-    sk.scramble = k.scramble;
     for (int l = 0; l <= 16; ++l) sk.tv_off[l] = 0;
     sk.g_tv = a->g_tv;
     if (tv_rec) {
@@ -3567,7 +2693,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
       }
       for (int l = a->tv->n_levels; l <= 16; ++l) sk.tv_off[l] = off;
     }
-    sk.slab = HN_SC_SLAB ? slab : nullptr;
+    sk.slab = slab;
     sk.dc = a->d_coarse;
     sk.df = a->d_fine;
     sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
@@ -3593,50 +2719,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
                        (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
     if ((st = hip_status(hipGetLastError()))) return st;
-#if HN_BR_PROF
-    {
-      unsigned long long f[8];
-      (void)hipStreamSynchronize(s);
-      (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_brprof), sizeof(f));
-      const double nb = (double)bg.nbins;
-      fprintf(stderr, "hn_br_profile cycles per bin: setup %.0f records %.0f overflow %.0f epilogue %.0f\n",
-              f[0] / nb, f[1] / nb, f[2] / nb, f[3] / nb);
-      memset(f, 0, sizeof(f));
-      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_brprof), f, sizeof(f));
-    }
-#endif
   }
-#if HN_PROFILE
-  {
-    unsigned long long ph[2][8];
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
-    for (int f = 0; f < 2; ++f)
-      fprintf(stderr, "hn_b1_profile %s waves=%llu cycles/wave: unit %.0f mlp %.0f scatter %.0f total %.0f\n",
-              f ? "waves1-2" : "wave0", ph[f][4], (double)ph[f][0] / ph[f][4], (double)ph[f][1] / ph[f][4],
-              (double)ph[f][2] / ph[f][4], (double)ph[f][3] / ph[f][4]);
-    memset(ph, 0, sizeof(ph));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph));
-    unsigned long long rg[5];
-    (void)hipMemcpyFromSymbol(rg, HIP_SYMBOL(g_ring), sizeof(rg));
-    fprintf(stderr, "hn_b1_ring per block: scatter wave total %.0f waiting %.0f cap-wait %.0f | MLP waves "
-            "slot-wait %.0f coarse-wait %.0f (per wave)\n", rg[0] / 256., rg[1] / 256., rg[4] / 256.,
-            rg[2] / (256. * kMW), rg[3] / (256. * kMW));
-    memset(rg, 0, sizeof(rg));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ring), rg, sizeof(rg));
-#if HN_TILE_PROF
-    unsigned long long tp[9];
-    (void)hipMemcpyFromSymbol(tp, HIP_SYMBOL(g_tile), sizeof(tp));
-    const double ntile = (double)a->n_rays * 8;   // 2 coarse + 6 fine tiles per ray
-    fprintf(stderr, "hn_b1_tile cycles/tile: F0 %.0f F1+F2G %.0f F3 %.0f dWc2+B4 %.0f B3+dWc1 %.0f "
-            "B2G+dWc0 %.0f B1+dWs1 %.0f B0+dWs0 %.0f\n", tp[0] / ntile, tp[1] / ntile, tp[2] / ntile,
-            tp[3] / ntile, tp[4] / ntile, tp[5] / ntile, tp[6] / ntile, tp[7] / ntile);
-    memset(tp, 0, sizeof(tp));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile), tp, sizeof(tp));
-#endif
-  }
-#endif
-  if (mode != kModeSplit || !HN_SC_SLAB) {
+  if (mode != kModeSplit) {
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(kSlabVBlocks), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,
                        a->d_coarse, a->d_fine, (a->d_table_mode & 2) ? 1 : 0);
     if ((st = hip_status(hipGetLastError()))) return st;
