@@ -104,18 +104,26 @@ def mfma_busy(ks, kernel, source):
             "grbm_gui_active": grbm, "source": source}
 
 
-def cpu_baseline(cfg, seconds=12.0, n_rays=256):
-    """Oracle (torch-CPU restatement of the reference) training step on a
-    bounded sample of the same workload: n_rays rays of the same scene shape,
-    same table size, fwd + bwd + RAdam; rays/s over >= 2 timed steps."""
+def cpu_baseline(cfg, steps=3, n_rays=None, warm_rays=256):
+    """Oracle (torch-CPU restatement of the reference) training step on the
+    config's own shape: n_rays = the config's N_rand rays per step (SURVEY
+    8(d): >= 3 timed steps at each config's B, after one warm-up step), same
+    table size, the config's loss terms (sparsity weight, TV on every step for
+    config 3, the bbox and background), fwd + bwd + RAdam.  The warm-up step
+    runs warm_rays rays (the same code path; it only pays first-call costs)."""
     import numpy as np
 
     from oracle import hashnerf_oracle as O
 
     threads = torch.get_num_threads()
+    n_rays = n_rays or cfg["N_rand"]
     T, finest = cfg["log2_hashmap_size"], cfg["finest_res"]
+    white = cfg.get("white_bkgd", True)
+    sparse_w = cfg.get("sparse_loss_weight", 1e-10)
+    tv_w = cfg["tv_loss_weight"] if cfg.get("tv_until", 1001) > 1001 else 0.0   # timed steps follow pretraining
     g = torch.Generator().manual_seed(0)
-    box = (torch.tensor([-4.02, -4.02, -3.34]), torch.tensor([4.02, 4.02, 3.24]))
+    box = tuple(torch.tensor(v) for v in cfg["bbox"]) if "bbox" in cfg else \
+        (torch.tensor([-4.02, -4.02, -3.34]), torch.tensor([4.02, 4.02, 3.24]))
     tab = ((torch.rand(16, 2 ** T, 2, generator=g) * 2 - 1) * 1e-4).requires_grad_(True)
     wc = {k: v.requires_grad_(True) for k, v in O.init_nerf_small(g).items()}
     wf = {k: v.requires_grad_(True) for k, v in O.init_nerf_small(g).items()}
@@ -126,17 +134,22 @@ def cpu_baseline(cfg, seconds=12.0, n_rays=256):
     focal = .5 * W / np.tan(.5 * 0.6911112070083618)
     K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])
 
-    def step(i):
+    def step(i, n):
         c2w = O.pose_spherical(float(i * 37 % 360 - 180), -30.0, 4.0)
         ro, rd = O.get_rays(H, W, K, c2w[:3, :4])
-        sel = torch.randperm(H * W, generator=g)[:n_rays]
+        sel = torch.randperm(H * W, generator=g)[:n]
         ro, rd = ro.reshape(-1, 3)[sel], rd.reshape(-1, 3)[sel]
         vd = rd / torch.norm(rd, dim=-1, keepdim=True)
-        rb = torch.cat([ro, rd, 2 * torch.ones(n_rays, 1), 6 * torch.ones(n_rays, 1), vd], -1)
+        rb = torch.cat([ro, rd, 2 * torch.ones(n, 1), 6 * torch.ones(n, 1), vd], -1)
         ret = O.render_rays(rb, wc, wf, tab, box[0], box[1], res, T,
-                            t_rand=torch.rand(n_rays, 64, generator=g),
-                            u=torch.rand(n_rays, 128, generator=g), white_bkgd=True)
-        loss = O.training_loss(ret, torch.rand(n_rays, 3, generator=g), 1e-10)
+                            t_rand=torch.rand(n, 64, generator=g),
+                            u=torch.rand(n, 128, generator=g), white_bkgd=white)
+        loss = O.training_loss(ret, torch.rand(n, 3, generator=g), sparse_w)
+        if tv_w:
+            for l in range(16):                        # run_nerf.py:628-635, loss.py:22-25
+                r, cube = O.tv_cube(l, 16, 16, finest)
+                mv = torch.randint(0, int(r - cube), (3,), generator=g)
+                loss = loss + tv_w * O.total_variation_loss(tab[l], l, mv, T, finest_res=finest)
         for p in params:
             p.grad = None
         loss.backward()
@@ -145,16 +158,15 @@ def cpu_baseline(cfg, seconds=12.0, n_rays=256):
                 O.radam_step(p, p.grad, m, v, i + 1, 0.01, weight_decay=1e-6 if p is not tab else 0.0,
                              eps=1e-15 if p is tab else 1e-8)
 
-    step(0)                                   # warm-up
+    step(0, warm_rays)                        # warm-up (first-call costs)
     t0 = time.perf_counter()
-    n = 0
-    while n < 2 or (time.perf_counter() - t0 < seconds and n < 20):
-        step(n + 1)
-        n += 1
+    for i in range(steps):
+        step(i + 1, n_rays)
     dt = time.perf_counter() - t0
-    return {"value": round(n * n_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle training steps x {n_rays} rays (T=2^{T}, finest {finest}, 64+128, "
-                      f"fwd+bwd+RAdam) on {threads} host threads, {dt:.1f} s"}
+    return {"value": round(steps * n_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} oracle training steps x {n_rays} rays (the config's B; T=2^{T}, finest {finest}, "
+                      f"64+128, fwd+bwd+RAdam{', TV' if tv_w else ''}) on {threads} host threads after a "
+                      f"{warm_rays}-ray warm-up step, {dt:.1f} s"}
 
 
 def _free_port():
@@ -194,7 +206,8 @@ def main():
                     help="uniform: random targets; procedural: train.procedural_field chair images")
     ap.add_argument("--pretrain", type=int, default=1000,
                     help="untimed training steps before warmup")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-steps", type=int, default=3,
+                    help="timed oracle steps of the CPU baseline, each at the config's N_rand")
     ap.add_argument("--ray-order", type=int, default=1, choices=(0, 1),
                     help="batch order from the sampler: 1 Morton order of the pixels, 0 draw order")
     ap.add_argument("--dense-table-step", action="store_true",
@@ -363,7 +376,7 @@ def main():
                                     atomic_peak_Greq_per_s=ATOMIC_PEAK_GREQ,
                                     atomic_frac=round(rate / ATOMIC_PEAK_GREQ, 3))
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg, seconds=args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(cfg, steps=args.cpu_steps)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

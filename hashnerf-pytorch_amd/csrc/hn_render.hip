@@ -1120,19 +1120,30 @@ struct BinW {
 __host__ __device__ inline int64_t sc_units_per_block(int64_t n_rays) {   // scatter_bins_kernel: 3 units per ray
   return (3 * (n_rays > 0 ? n_rays : 1) + kBwdBlocks - 1) / kBwdBlocks;
 }
-__host__ __device__ inline size_t ovf_per_block(int64_t n_rays) { return (size_t)sc_units_per_block(n_rays) * 64 * 64; }
+// TV records (the scatter blocks' share of the x-pairs, cubes <= kTvRecMaxCube):
+// at most L x ((c + 2) / 2) x (c + 1)^2 pairs over the 256 blocks
+constexpr int kTvRecMaxCube = 50;
+constexpr size_t kTvRecPerBlock = (16 * ((kTvRecMaxCube + 2) / 2) * (kTvRecMaxCube + 1) * (kTvRecMaxCube + 1) +
+                                   kBwdBlocks - 1) / kBwdBlocks;
+// a producer's overflow list holds everything it can write: its units' render
+// records (64 samples x 16 levels x 4 corner rows each) plus its TV share
+__host__ __device__ inline size_t ovf_per_block(int64_t n_rays) {
+  return (size_t)sc_units_per_block(n_rays) * 64 * 64 + kTvRecPerBlock;
+}
 __host__ __device__ inline size_t bin_records(int nbins, int cap, int64_t n_rays) {
   return (size_t)kBwdBlocks * nbins * cap + (size_t)kBwdBlocks * ovf_per_block(n_rays);
 }
 // Overflow book, u32 words after the counts and level maxima (idx + nrec +
 // kBwdBlocks * (nbins + 16)): total spilled, spilled per bin, placement
-// cursors, first slot per bin, spilled per producer block, record ids
-// (relative to the first overflow record) bucketed by bin.
+// cursors, first slot per bin, the scatter blocks' slab-block counter,
+// spilled per producer block, record ids (relative to the first overflow
+// record) bucketed by bin.  All of it lives in the call's workspace, so
+// concurrent hn_render_bwd calls with their own workspaces share nothing.
 struct OvfBook {
-  uint32_t *cnt, *per_bin, *cur, *first, *blk, *ids;
+  uint32_t *cnt, *per_bin, *cur, *first, *slab_next, *blk, *ids;
 };
 __host__ __device__ inline size_t ovf_book_words(int nbins, int64_t n_rays) {
-  return 1 + 3 * (size_t)nbins + kBwdBlocks + (size_t)kBwdBlocks * ovf_per_block(n_rays);
+  return 2 + 3 * (size_t)nbins + kBwdBlocks + (size_t)kBwdBlocks * ovf_per_block(n_rays);
 }
 __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbins) {
   OvfBook o;
@@ -1140,7 +1151,8 @@ __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbin
   o.per_bin = o.cnt + 1;
   o.cur = o.per_bin + nbins;
   o.first = o.cur + nbins;
-  o.blk = o.first + nbins;
+  o.slab_next = o.first + nbins;
+  o.blk = o.slab_next + 1;
   o.ids = o.blk + kBwdBlocks;
   return o;
 }
@@ -1316,7 +1328,6 @@ struct ScK {
   hn_mlp_grad dc, df;
   int32_t overwrite_mlp;
 };
-__device__ unsigned int g_slab_next;   // next slab block for the scatter blocks
 constexpr int kScWaves = 16;
 constexpr int kScMaxBinsLog2 = 13;
 constexpr int kScMaxBins = 1 << kScMaxBinsLog2;   // LDS counters (32 KiB): T <= 22 at 2^13 entries per bin
@@ -1579,7 +1590,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     for (;;) {
       __syncthreads();   // part and vb_sh are free (the pool's last readers, or the previous combine)
       if (threadIdx.x == 0)
-        vb_sh = (int)__hip_atomic_fetch_add(&g_slab_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vb_sh = (int)__hip_atomic_fetch_add(ob.slab_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       const int vb = vb_sh;
       if (vb >= kSlabVBlocks) break;
@@ -1882,7 +1893,7 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
     const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
     uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
     for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
-    if (threadIdx.x == 0) g_slab_next = 0u;   // the scatter kernel's slab-block counter
+    if (threadIdx.x == 0) o[1 + 3 * k.nbins] = 0u;   // the scatter kernel's slab-block counter (ob.slab_next)
   }
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
@@ -2632,7 +2643,9 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     int nbf, nbb;
     if ((st = make_tv(a->tv, tvk, nbf, nbb))) return st;
     if (a->tv->n_levels != cfg->grid.n_levels || a->tv->log2_hashmap_size != T) return HN_E_SHAPE;
-    if (mode == kModeSplit) {
+    bool small = a->tv->n_levels <= 16;
+    for (int l = 0; l < a->tv->n_levels && small; ++l) small = a->tv->cube[l] <= kTvRecMaxCube;
+    if (mode == kModeSplit && small) {   // the overflow lists hold these records (ovf_per_block)
       tv_rec = true;
     } else {
       if (a->table_step || !a->d_table) return HN_E_SHAPE;

@@ -120,6 +120,13 @@ class RAdam(Optimizer):
         return int(getattr(p, "_hn_levels", 0) or 0)
 
     def state_dict(self):
+        xchg = getattr(self, "sharded_state", None)
+        if xchg is not None and xchg.stale:
+            # data-parallel sharded table step (train.ShardedTableStep): the
+            # table's moments live on the ranks' shards; the full-size copy
+            # here is out of date until every rank has gathered them
+            raise RuntimeError("RAdam.state_dict: the hash table's moments are sharded over the ranks and the "
+                               "optimizer's copy is stale; call Trainer.sync_optimizer_state() on every rank first")
         sd = super().state_dict()
         if not any(self._levels(p) for g in self.param_groups for p in g["params"]):
             return sd

@@ -126,6 +126,43 @@ def allreduce_grads(table, mlp_params, group=None, live=None):
         off += n
 
 
+class Collectives:
+    """The two collectives of the sharded table step with RCCL's calling
+    convention: ``reduce_scatter(out, inp)`` = ``reduce_scatter_tensor``
+    (SUM; ``out`` is this rank's 1/world slice of ``inp``'s sum) and
+    ``all_gather(out, inp)`` = ``all_gather_into_tensor`` (``inp`` may be
+    ``out``'s own slice: in place).  On gloo, which has neither, each is
+    emulated INTO THE SAME out tensor (all-reduce + copy of the rank's slice;
+    a list all-gather over ``out``'s views), so the offsets, views and
+    out-tensors that the RCCL run uses are exactly what a gloo test runs --
+    only the transport differs (``inp`` of a gloo reduce_scatter is left
+    holding the full sum; the RCCL call leaves it untouched, and the step
+    never reads it again)."""
+
+    def __init__(self, rank, world, group=None, emulate=None):
+        self.rank, self.world, self.group = rank, world, group
+        self.emulate = dist.get_backend(group) == "gloo" if emulate is None else emulate
+
+    def reduce_scatter(self, out, inp):
+        n = out.numel()
+        if inp.numel() != n * self.world:
+            raise ValueError(f"reduce_scatter: input {inp.numel()} != {self.world} x output {n}")
+        if self.emulate:
+            dist.all_reduce(inp, group=self.group)
+            out.copy_(inp[self.rank * n:(self.rank + 1) * n])
+        else:
+            dist.reduce_scatter_tensor(out, inp, group=self.group)
+
+    def all_gather(self, out, inp):
+        n = inp.numel()
+        if out.numel() != n * self.world:
+            raise ValueError(f"all_gather: output {out.numel()} != {self.world} x input {n}")
+        if self.emulate:
+            dist.all_gather(list(out.chunk(self.world)), inp.clone(), group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+
+
 class ShardedTableStep:
     """Data-parallel exchange + RAdam step of the hash table as reduce-scatter
     -> RAdam on this rank's shard -> all-gather (SURVEY 8e's alternative to
@@ -143,13 +180,20 @@ class ShardedTableStep:
     tail on -- contiguous, no copy of the 60 MB tail.  The table parameter is
     re-pointed into the parameter buffer, so the all-gather (in place) updates
     the tail directly and the coarse live rows are scattered back (4 MB).
-    The table's RAdam moments exist for this rank's shard only;
-    gather_state() rebuilds the full ones (dead rows: zero, as the dense
-    reference keeps them) for a checkpoint."""
 
-    def __init__(self, table, live, rank, world, group=None):
+    The table's RAdam moments live for this rank's shard only.  They start
+    from ``state`` (the optimizer's exp_avg / exp_avg_sq of the table, e.g.
+    loaded from a checkpoint, run_nerf.py:158-168), packed like the gradient;
+    gather_state() rebuilds the full ones (dead rows: zero, as the dense
+    reference keeps them).  ``stale`` is set by every step and cleared by
+    gather_state(): RAdam.state_dict() refuses to write a checkpoint while the
+    optimizer's full-size copy is stale (Trainer.sync_optimizer_state)."""
+
+    def __init__(self, table, live, rank, world, group=None, state=None, stepper=None):
         L_, R, F_ = table.shape
         self.table, self.rank, self.world, self.group = table, rank, world, group
+        self.coll = Collectives(rank, world, group)
+        self.stepper = HF.radam_step if stepper is None else stepper
         self.full = L_ * R * F_
         n_lv, rows = live if live is not None else (0, None)
         self.rows = rows
@@ -161,12 +205,29 @@ class ShardedTableStep:
         dev = table.device
         self.gbuf = torch.zeros(self.head + self.P, dtype=torch.float32, device=dev)
         self.pbuf = torch.zeros(self.head + self.P, dtype=torch.float32, device=dev)
+        self.g_shard = torch.empty(self.s, dtype=torch.float32, device=dev)
         with torch.no_grad():
             self.pbuf[:self.full].copy_(table.data.reshape(-1))
         table.data = self.pbuf[:self.full].view(L_, R, F_)
         self.m = torch.zeros(self.s, dtype=torch.float32, device=dev)
         self.v = torch.zeros(self.s, dtype=torch.float32, device=dev)
-        self.gloo = dist.get_backend(group) == "gloo"
+        if state is not None and "exp_avg" in state:
+            with torch.no_grad():
+                self.m.copy_(self._shard_of(state["exp_avg"]))
+                self.v.copy_(self._shard_of(state["exp_avg_sq"]))
+        self.stale = False
+
+    def _shard_of(self, full):
+        """This rank's slice of a full-size table tensor packed like the
+        exchanged gradient ([dense tail | coarse live rows | zero pad])."""
+        F_ = self.table.shape[2]
+        flat = full.detach().reshape(-1).to(device=self.pbuf.device, dtype=torch.float32)
+        parts = [flat[self.head:]]
+        if self.nc:
+            parts.append(flat[:self.head].view(-1, F_).index_select(0, self.rows).reshape(-1))
+        packed = torch.cat(parts)
+        packed = torch.cat([packed, packed.new_zeros(self.P - packed.numel())])
+        return packed[self.rank * self.s:(self.rank + 1) * self.s]
 
     def grad_view(self):
         """Where the render backward writes the table gradient (overwrite)."""
@@ -184,24 +245,14 @@ class ShardedTableStep:
         if self.nc:
             torch.index_select(self.gbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.gbuf))
             torch.index_select(self.pbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.pbuf))
-        packed_g = self.gbuf[self.head:]
         lo = self.head + self.rank * self.s
-        if self.gloo:      # gloo has no reduce-scatter: the rehearsal all-reduces and slices
-            dist.all_reduce(packed_g, group=self.group)
-            g_shard = self.gbuf[lo:lo + self.s]
-        else:
-            g_shard = torch.empty(self.s, dtype=torch.float32, device=self.gbuf.device)
-            dist.reduce_scatter_tensor(g_shard, packed_g, group=self.group)
+        self.coll.reduce_scatter(self.g_shard, self.gbuf[self.head:])
         p_shard = self.pbuf[lo:lo + self.s]
-        HF.radam_step([(p_shard, g_shard, self.m, self.v, coeffs)])
-        if self.gloo:
-            parts = list(self.pbuf[self.head:].chunk(self.world))
-            mine = p_shard.clone()
-            dist.all_gather(parts, mine, group=self.group)
-        else:
-            dist.all_gather_into_tensor(self.pbuf[self.head:], p_shard, group=self.group)
+        self.stepper([(p_shard, self.g_shard, self.m, self.v, coeffs)])
+        self.coll.all_gather(self.pbuf[self.head:], p_shard)
         if self.nc:
             self.pbuf[:self.head].view(-1, F_).index_copy_(0, self.rows, self._packed_coarse(self.pbuf))
+        self.stale = True
 
     @torch.no_grad()
     def gather_state(self):
@@ -210,16 +261,14 @@ class ShardedTableStep:
         F_ = self.table.shape[2]
         for sh in (self.m, self.v):
             packed = torch.empty(self.P, dtype=torch.float32, device=sh.device)
-            if self.gloo:
-                dist.all_gather(list(packed.chunk(self.world)), sh.clone(), group=self.group)
-            else:
-                dist.all_gather_into_tensor(packed, sh, group=self.group)
+            self.coll.all_gather(packed, sh)
             full = torch.zeros(self.full, dtype=torch.float32, device=sh.device)
             full[self.head:] = packed[:self.full - self.head]
             if self.nc:
                 full[:self.head].view(-1, F_).index_copy_(0, self.rows,
                                                           packed[self.full - self.head:][:self.nc].view(-1, F_))
             out.append(full.view(self.table.shape))
+        self.stale = False
         return out
 
 
@@ -517,7 +566,11 @@ class Trainer:
         # the ranks (ShardedTableStep); the backward writes into its buffer
         self._xchg = None
         if self.world > 1 and self.dp_sharded:
-            self._xchg = ShardedTableStep(table, self._live_rows(), self.rank, self.world)
+            # the moments continue from the optimizer's (a resumed run's
+            # checkpoint, or an earlier setup's gathered state)
+            self._xchg = ShardedTableStep(table, self._live_rows(), self.rank, self.world,
+                                          state=self.optimizer.state.get(table))
+            self.optimizer.sharded_state = self._xchg
             self._gtable = self._xchg.grad_view()
         else:
             self._gtable = torch.zeros_like(table)

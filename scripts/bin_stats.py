@@ -58,7 +58,9 @@ def main():
     shift, nbins, cap = bin_geom(T, n)
     off = 2 * G_END + BLOCKS * 4 * W_END + n * 64 * 32 + n * 256 * 4
     off += n * 192 * 32                       # fine feature grads (binned schedule)
-    nrec = BLOCKS * nbins * cap + n * 192 * 64   # regions + overflow (ovf_records)
+    tv_per_block = (16 * 26 * 51 * 51 + BLOCKS - 1) // BLOCKS     # hn_render.hip kTvRecPerBlock
+    ovf_per_block = (3 * n + BLOCKS - 1) // BLOCKS * 64 * 64 + tv_per_block
+    nrec = BLOCKS * nbins * cap + BLOCKS * ovf_per_block   # regions + overflow lists (hn_render.hip bin_records)
     ws = st.wsb.view(torch.int32)
     idx0 = off + 4 * nrec
     cnt = ws[idx0 + nrec: idx0 + nrec + BLOCKS * nbins].cpu().numpy().astype(np.int64).reshape(nbins, BLOCKS)

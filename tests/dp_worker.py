@@ -46,10 +46,14 @@ def main(batch_path, out_path):
     dist.destroy_process_group()
 
 
-def train(out_path, sharded, steps):
+def train(out_path, sharded, steps, resume_at=0):
     """`steps` training steps of the explicit trainer on this rank's own draws,
     the table exchange sharded (reduce-scatter / shard RAdam / all-gather) or
-    all-reduced; rank 0 saves the table, its RAdam moments and the MLP weights."""
+    all-reduced; rank 0 saves the table, its RAdam moments and the MLP weights.
+    resume_at > 0: after that many steps the moments are gathered into the
+    optimizer (a checkpoint's state, run_nerf.py:663-680) and the sharded
+    exchange is rebuilt from it, as a resumed run builds it (create_nerf's
+    reload, run_nerf_helpers.py:158-168)."""
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
     import hn_loader
@@ -60,7 +64,11 @@ def train(out_path, sharded, steps):
     args = default_args(N_rand=256, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=4, sparse_loss_weight=1e-3)
     tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)
     tr.dp_sharded = sharded
-    for _ in range(steps):
+    for k in range(steps):
+        if resume_at and k == resume_at:
+            tr.sync_optimizer_state()
+            tr.optimizer.state_dict()          # refuses stale moments: must not raise now
+            tr._grads = tr._xchg = None        # the next step rebuilds the exchange from optimizer.state
         tr.step()
     tr.sync_optimizer_state()
     torch.cuda.synchronize()
@@ -78,6 +86,6 @@ def train(out_path, sharded, steps):
 
 if __name__ == "__main__":
     if sys.argv[1] == "train":
-        train(sys.argv[2], sys.argv[3] == "1", int(sys.argv[4]))
+        train(sys.argv[2], sys.argv[3] == "1", int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 0)
     else:
         main(sys.argv[1], sys.argv[2])

@@ -185,3 +185,94 @@ def test_live_pair_mask_matches_live_rows():
         expect = np.zeros(n_lv << (T - 1), dtype=bool)
         expect[rows.numpy() >> 1] = True
         assert np.array_equal(bits, expect)
+
+
+def _toy_step(tensors):
+    """A per-element stand-in for hn_radam_step (test infrastructure): the
+    sharded step's index math does not depend on the update's form, and
+    p, m, v stay untouched where g = m = v = 0 (the dead rows), as RAdam's do."""
+    for p, g, m, v, c in tensors:
+        m.mul_(c["beta1"]).add_(g)
+        v.mul_(c["beta2"]).addcmul_(g, g)
+        p.sub_(c["lr"] * m / (v.sqrt() + 1.0))
+
+
+def _sharded_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import ShardedTableStep
+    L_, R, F_ = 4, 64, 2
+    g0 = torch.Generator().manual_seed(11)
+    rows = torch.tensor([0, 3, 5, 17, 40, 63, 64 + 2, 64 + 9, 64 + 33], dtype=torch.int64)   # levels 0-1 sparse
+    live = (2, rows)
+    dead = torch.ones(2 * R, dtype=torch.bool)
+    dead[rows] = False
+    p0 = torch.randn(L_, R, F_, generator=g0)
+    m0 = torch.randn(L_, R, F_, generator=g0)
+    v0 = torch.rand(L_, R, F_, generator=g0)
+    m0[:2] = m0[:2].reshape(-1, F_).masked_fill(dead[:, None], 0).view(2, R, F_)
+    v0[:2] = v0[:2].reshape(-1, F_).masked_fill(dead[:, None], 0).view(2, R, F_)
+    c = {"beta1": 0.9, "beta2": 0.99, "lr": 0.05}
+
+    def grads(step):
+        out = []
+        for r in range(world):
+            g = torch.randn(L_, R, F_, generator=torch.Generator().manual_seed(100 * step + r))
+            g[:2] = g[:2].reshape(-1, F_).masked_fill(dead[:, None], 0).view(2, R, F_)
+            out.append(g)
+        return out
+
+    # sharded: RCCL's call sequence, the collectives emulated on gloo
+    table = torch.nn.Parameter(p0.clone())
+    xs = ShardedTableStep(table, live, rank, world, state={"exp_avg": m0, "exp_avg_sq": v0},
+                          stepper=_toy_step)
+    assert xs.coll.emulate
+    for step in range(3):
+        xs.grad_view().copy_(grads(step)[rank])
+        xs.step(c)
+    assert xs.stale
+    m, v = xs.gather_state()
+    assert not xs.stale
+    # reference: the summed gradient, the dense update over the whole table
+    pr, mr, vr = p0.clone(), m0.clone(), v0.clone()
+    for step in range(3):
+        _toy_step([(pr, sum(grads(step)), mr, vr, c)])
+    if rank == 0:
+        torch.save({"p": table.detach().clone(), "m": m, "v": v, "pr": pr, "mr": mr, "vr": vr}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_table_step_matches_dense(tmp_path):
+    """train.ShardedTableStep through train.Collectives (gloo emulating
+    reduce_scatter_tensor / all_gather_into_tensor into the RCCL call's own
+    out-tensors and offsets): 3 steps from loaded moments (a resumed run) leave
+    the table and the gathered moments equal to the summed-gradient dense
+    update; the dead coarse rows stay untouched."""
+    port = _free_port()
+    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path / "sh.pt")), nprocs=2, join=True)
+    got = torch.load(tmp_path / "sh.pt", weights_only=True)
+    torch.testing.assert_close(got["p"], got["pr"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(got["m"], got["mr"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(got["v"], got["vr"], rtol=1e-6, atol=1e-7)
+
+
+def test_sharded_state_dict_refuses_stale_moments():
+    """RAdam.state_dict() raises while a sharded table step holds newer
+    moments than the optimizer (a checkpoint would silently keep stale ones)."""
+    import sys
+    import types
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn = hn_loader.load()
+    p = torch.nn.Parameter(torch.zeros(4))
+    opt = hn.RAdam([p], lr=0.1)
+    opt.sharded_state = types.SimpleNamespace(stale=True)
+    with pytest.raises(RuntimeError, match="sync_optimizer_state"):
+        opt.state_dict()
+    opt.sharded_state.stale = False
+    opt.state_dict()

@@ -36,12 +36,12 @@ def _free_port():
     return p
 
 
-def _trainer(hn, n_rand, **over):
+def _trainer(hn, n_rand, HW=64, **over):
     from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
     spec_args = dict(N_rand=n_rand, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=10 ** 6,
                      sparse_loss_weight=1e-3)
     spec_args.update(over)
-    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
+    data = SyntheticBlender(HW, HW, 4, DEV, seed=0)
     tr = Trainer(default_args(**spec_args), data, DEV, seed=0)
     tr.fuse_table_step = False
     return tr, spec_args
@@ -81,30 +81,44 @@ def test_dp_sharded_table_step_equals_allreduce(hn, tmp_path):
     rank's shard -> all-gather, train.ShardedTableStep) leaves the table, its
     gathered RAdam moments and the MLP weights bitwise equal to the all-reduce
     + full RAdam path (two-rank sums are order-free; the per-element update is
-    the same kernel)."""
+    the same kernel).  The collectives run RCCL's calls (reduce_scatter_tensor
+    into the shard, in-place all_gather_into_tensor into the parameter
+    buffer), emulated on gloo into the same out-tensors (train.Collectives).
+    The second sharded run resumes after 7 steps: the moments are gathered
+    into the optimizer, the exchange is rebuilt from them, and the run ends
+    bitwise where the uninterrupted all-reduce run does (the moments must
+    carry over: from zero, step 8's update would differ)."""
     res = {}
-    for sharded in (1, 0):
-        out = str(tmp_path / f"train_{sharded}.pt")
-        _launch(["train", out, str(sharded), "8"])
-        res[sharded] = torch.load(out, weights_only=True)
-    a, b = res[1], res[0]
-    assert a["step"] == b["step"] == 8
-    for k in ("table", "m", "v"):
-        assert torch.equal(a[k], b[k]), k
-    assert torch.count_nonzero(a["m"]) > 0
-    for x, y in zip(a["mlp"], b["mlp"]):
-        assert torch.equal(x, y)
+    for name, args in (("sharded", ["1", "8"]), ("allreduce", ["0", "8"]), ("resumed", ["1", "8", "7"])):
+        out = str(tmp_path / f"train_{name}.pt")
+        _launch(["train", out] + args)
+        res[name] = torch.load(out, weights_only=True)
+    b = res["allreduce"]
+    for name in ("sharded", "resumed"):
+        a = res[name]
+        assert a["step"] == b["step"] == 8
+        for k in ("table", "m", "v"):
+            assert torch.equal(a[k], b[k]), (name, k)
+        assert torch.count_nonzero(a["m"]) > 0
+        for x, y in zip(a["mlp"], b["mlp"]):
+            assert torch.equal(x, y), name
 
 
-def test_dp_two_ranks_equal_global_batch(hn, tmp_path):
-    tr, spec_args = _trainer(hn, 512)
-    i = 1
+@pytest.mark.parametrize("B,T,HW,i", [(512, 14, 64, 1), (16384, 19, 200, 501)],
+                         ids=["small", "config4_rank_shape"])
+def test_dp_two_ranks_equal_global_batch(hn, tmp_path, B, T, HW, i):
+    """Two ranks on halves of a global batch: the SUM exchange of their
+    gradients = the one-rank gradient of the whole batch (relative 1e-5).
+    config4_rank_shape: BASELINE configs[3]'s per-rank shape (T=19, finest
+    512, 8,192 rays per rank; configs/hotdog.txt) against the one-rank
+    16,384-ray gradient, full image (i > precrop_iters), TV on rank 0."""
+    tr, spec_args = _trainer(hn, B, log2_hashmap_size=T, HW=HW)
     batch = tr.draw_batch(i)
-    assert batch["tv"] is not None
+    assert batch["tv"] is not None and batch["rays"].shape[0] == B
     tr._fused_forward_backward(i, batch)
     torch.cuda.synchronize()
     g_table, g_mlp = _grads(tr)
-    world, B = 2, 512
+    world = 2
     ranks = []
     for r in range(world):
         sl = slice(r * B // world, (r + 1) * B // world)
@@ -112,7 +126,7 @@ def test_dp_two_ranks_equal_global_batch(hn, tmp_path):
         if r == 0:                                    # TV counted once (train.dp_loss)
             d["tv_cubes"], d["tv_mv"] = list(batch["tv"][0]), batch["tv"][1].cpu()
         ranks.append(d)
-    spec = dict(H=64, W=64, n_img=4, args=spec_args, i=i, ranks=ranks)
+    spec = dict(H=HW, W=HW, n_img=4, args=spec_args, i=i, ranks=ranks)
     bpath, opath = str(tmp_path / "batch.pt"), str(tmp_path / "dp_out.pt")
     torch.save(spec, bpath)
     port = _free_port()
