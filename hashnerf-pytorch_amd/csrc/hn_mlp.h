@@ -119,16 +119,24 @@ struct MlpAct {
 // mask bits of one ReLU'd D-layout block: its values are +0 or positive, so a
 // bit is (bits + 0x7fffffff) >> 31 (integer ops only: the compare forms, which
 // min(bits, 1) also becomes, hold lane masks in SGPR pairs and spilled the forward)
+// Two ops per value: t = 0 - bits has bit 31 set iff bits >= 1 (a ReLU'd value
+// is +0 or positive, so bits < 2^31), and (m << 1) | (t >> 31) is one
+// v_alignbit_b32 that shifts the word's bits up and inserts the new one at
+// bit 0 -- so r runs from 15 down and bit r ends at position r.
 HN_DEV void relu_mask_or(const f32x16& v, uint32_t& m, int ob) {
+  uint32_t w = 0u;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    m |= ((__float_as_uint(v[r]) + 0x7fffffffu) >> 31) << (16 * ob + r);
-  }
+  for (int r = 15; r >= 0; --r) w = __builtin_amdgcn_alignbit(w, 0u - __float_as_uint(v[r]), 31u);
+  m |= w << (16 * ob);
 }
 
+// ReLU as one integer max on the bits (a negative float or -0 is a negative
+// int32): equal to v > 0 ? v : +0 for every non-NaN v, and one v_max_i32
+// where the float form is a v_max_f32 plus the IEEE-mode canonicalisation of
+// its input; a NaN passes through, as in torch.relu.
 HN_DEV void relu16(f32x16& v) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+  for (int r = 0; r < 16; ++r) v[r] = __int_as_float(max(__float_as_int(v[r]), 0));
 }
 HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 0)
 #pragma unroll
@@ -146,6 +154,9 @@ HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0I
                             MlpAct& a, f32x16& c2, int lane) {
   a.m[0] = a.m[1] = a.m[2] = 0u;
   // sigma_net.0: 32 -> 64, ReLU
+  // (Both output blocks of a GEMM sharing one B split per chunk, as the
+  // backward's gemm_w2 does, measured slower here: render_fwd_kernel 0.300 ->
+  // 0.307 ms, more spills at 4 waves per SIMD; r04c.)
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
     a.h0[ob] = gemm<R_F0>(P, ob, zero16(), lane, [&](int s) { return feat[s]; });

@@ -338,4 +338,77 @@ HN_DEV void rank_sort_wave(const float* src, float* dst, int S, int lane, uint8_
   lds_fence_wave();
 }
 
+// float <-> uint32 key with the same order (negative floats reversed); -0
+// maps to +0's key, so equal floats have equal keys.
+HN_DEV uint32_t sort_key(float v) {
+  uint32_t b = __float_as_uint(v);
+  if (b == 0x80000000u) b = 0u;
+  return b ^ ((b >> 31) ? 0xffffffffu : 0x80000000u);
+}
+HN_DEV float key_value(uint32_t k) { return __uint_as_float(k ^ ((k >> 31) ? 0x80000000u : 0xffffffffu)); }
+
+// The same result as rank_sort_wave(src, dst, 192, lane, origin, 64) -- the
+// values torch.sort returns, and origin[rank] = the coarse index or 255 --
+// for src = [64 coarse z, non-decreasing | 128 importance z]: the importance
+// samples are sorted by a bitonic network over the wave (2 per lane, cross-
+// lane exchanges by ds_bpermute), then each element's rank is its position in
+// its own run plus a binary search in the other run (coarse before importance
+// on ties, as the rank sort's index tie-break puts them; ties among importance
+// samples are equal values tagged 255, so their order is not observable).
+// ~0.5 k instructions per wave where the rank sort's 192 x 192 compares take
+// ~3 k.  Returns false (dst untouched) when the coarse run is not sorted.
+HN_DEV bool merge_sort_z(const float* src, float* dst, float* tmp, int lane, uint8_t* origin) {
+  const float zc = src[lane];
+  const float zn = lane < 63 ? src[lane + 1] : zc;
+  if (__ballot(sort_key(zn) < sort_key(zc)) != 0ull) return false;
+  uint32_t k[2] = {sort_key(src[64 + lane]), sort_key(src[128 + lane])};
+#pragma unroll
+  for (int kk = 2; kk <= 128; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      if (j == 64) {   // partner in the other register of this lane (kk = 128: ascending)
+        const uint32_t lo = min(k[0], k[1]), hi = max(k[0], k[1]);
+        k[0] = lo;
+        k[1] = hi;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int i = lane + 64 * r;
+          const uint32_t kp = shfl_from(k[r], lane ^ j);
+          const bool asc = (i & kk) == 0, lower = (i & j) == 0;
+          k[r] = (lower == asc) ? min(k[r], kp) : max(k[r], kp);
+        }
+      }
+    }
+  }
+  tmp[lane] = key_value(k[0]);
+  tmp[64 + lane] = key_value(k[1]);
+  lds_fence_wave();
+  // coarse e: e + #{importance < v} (lower bound in the sorted importance run)
+  {
+    const uint32_t kc = sort_key(zc);
+    int lo = 0, hi = 128;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sort_key(tmp[mid]) < kc) lo = mid + 1; else hi = mid;
+    }
+    dst[lane + lo] = zc;
+    if (origin) origin[lane + lo] = (uint8_t)lane;
+  }
+  // importance at sorted position p: p + #{coarse <= v} (upper bound in the coarse run)
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int p = lane + 64 * r;
+    int lo = 0, hi = 64;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sort_key(src[mid]) <= k[r]) lo = mid + 1; else hi = mid;
+    }
+    dst[p + lo] = key_value(k[r]);
+    if (origin) origin[p + lo] = (uint8_t)255;
+  }
+  lds_fence_wave();
+  return true;
+}
+
 }  // namespace hn

@@ -158,6 +158,10 @@ constexpr int kGsRcp = 48, kGsLds = 96;
 // levels tile_level(m, h), m = 0..7).  hash_encoding.py:84-110.
 HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __restrict__ table, const float pt[3], int h,
                         f32x16& feat) {
+  // (Software-pipelining the levels -- level m + 1 or m + 2's gathers issued
+  // before level m's are consumed -- measured slower: render_fwd_kernel 0.310
+  // -> 0.330 / 0.323 ms, r04b; the other three waves of the SIMD already hide
+  // the gathers' latency.)
   float xc[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], g.bmin[a], g.bmax[a]);
@@ -171,7 +175,7 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     Voxel v;
     voxel_level_rcp(pt, xc, gs, rg, g.bmin, mask, v);
     float f0, f1;
-    encode_level_off(table, l << g.log2T, v, f0, f1);
+    encode_level_xpair(table, l << g.log2T, v, f0, f1);   // r04c: 0.2966 -> 0.2959 ms vs encode_level_off
     feat[2 * m] = f0;
     feat[2 * m + 1] = f1;
     if (m & 1) __builtin_amdgcn_sched_barrier(0);   // <= 16 gathers in flight
@@ -208,6 +212,24 @@ constexpr int kFZc = 0, kFZsrc = 64, kFZs = 256, kFRaw = 448, kFW = 1216, kFBins
 // loops): one ray per wave, so a 4096-ray batch is exactly one round on 256
 // CUs (3 waves: 0.427 ms, a 1/3-occupied second round; 4: 0.418 ms)
 
+// Diagnostic phase timers of the forward (HN_PROFILE=1 builds only; never in
+// the shipped library): shader-clock cycles per wave in [0] coarse encode,
+// [1] coarse MLP + stores, [2] composite + sampling + sort, [3] fine encode,
+// [4] fine MLP + stores, [5] final composite, [6] total, [7] waves; printed by
+// hn_render_fwd after a synchronising read.  The encode laps wait for the
+// features first, so a gather's latency counts in its encode phase.
+#ifndef HN_PROFILE
+#define HN_PROFILE 0
+#endif
+#if HN_PROFILE
+__device__ unsigned long long g_fwd_prof[8];
+#define HN_FT(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); ft[i] += n_ - t_; t_ = n_; } while (0)
+#define HN_FT_FEAT(i, f) do { asm volatile("" ::"v"((f)[0]), "v"((f)[15])); HN_FT(i); } while (0)
+#else
+#define HN_FT(i) ((void)0)
+#define HN_FT_FEAT(i, f) ((void)0)
+#endif
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
 void render_fwd_kernel(RenderK k) {
   __shared__ __attribute__((aligned(16))) float smem[kFwdWaves * kFLds + kGsLds];
@@ -223,6 +245,11 @@ void render_fwd_kernel(RenderK k) {
   const int64_t grp = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
   const int64_t ray = grp * kFwdWaves + wave;
   if (ray >= k.B) return;
+#if HN_PROFILE
+  uint64_t ft[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+  uint64_t t_ = t0_;
+#endif
   float* L = smem + wave * kFLds;
   float* zc = L + kFZc;
   float* zsrc = L + kFZsrc;
@@ -266,6 +293,7 @@ void render_fwd_kernel(RenderK k) {
     ray_point(r, zc[q], pt);
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
+    HN_FT_FEAT(0, feat);
     if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
     MlpAct a;
     f32x16 c2;
@@ -276,6 +304,7 @@ void render_fwd_kernel(RenderK k) {
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
       *reinterpret_cast<float4*>(k.raw_c + (ray * kSc + q) * 4) = o4;
     }
+    HN_FT(1);
   }
   lds_fence_wave();
   CompOut co;
@@ -301,12 +330,18 @@ void render_fwd_kernel(RenderK k) {
     const double var = wave_sum(d0 * d0 + d1 * d1) / kNi;
     if (lane == 0) k.z_std[ray] = (float)sqrt(var);
   }
-  rank_sort_wave(zsrc, zs, kSf, lane, k.fine_src + ray * kSf, kSc);
+  // sort(cat(z_vals, z_samples)) (:551): a merge of the sorted coarse run with
+  // the bitonic-sorted importance samples (rawb is free until the fine tiles),
+  // the all-pairs rank sort if the coarse run is ever out of order
+  // (render_fwd_kernel 0.2998 -> 0.2966 ms, r04c)
+  if (!merge_sort_z(zsrc, zs, rawb, lane, k.fine_src + ray * kSf))
+    rank_sort_wave(zsrc, zs, kSf, lane, k.fine_src + ray * kSf, kSc);
   for (int i = lane; i < kSf; i += 64) k.z_fine[ray * kSf + i] = zs[i];
 
   // ---- fine network (:556) ----
   c0sh_lds_store(opaque_ptr(k.Pf), sh8, c0l, lane);   // the coarse tiles' reads are done (in-order LDS)
   lds_fence_wave();
+  HN_FT(2);
   for (int tau = 0; tau < kSf / 32; ++tau) {
     const float* P = opaque_ptr(k.Pf);
     const int q = 32 * tau + p;
@@ -314,6 +349,7 @@ void render_fwd_kernel(RenderK k) {
     ray_point(r, zs[q], pt);
     f32x16 feat;
     encode_tile(k.g, gsl, k.table, pt, h, feat);
+    HN_FT_FEAT(3, feat);
     if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
     MlpAct a;
     f32x16 c2;
@@ -324,6 +360,7 @@ void render_fwd_kernel(RenderK k) {
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
       *reinterpret_cast<float4*>(k.raw_f + (ray * kSf + q) * 4) = o4;
     }
+    HN_FT(4);
   }
   lds_fence_wave();
   CompOut fo;
@@ -336,6 +373,13 @@ void render_fwd_kernel(RenderK k) {
     k.acc[ray] = fo.acc;
     k.sparsity[ray] = fo.entropy;
   }
+#if HN_PROFILE
+  HN_FT(5);
+  ft[6] = __builtin_amdgcn_s_memtime() - t0_;
+  ft[7] = 1;
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_fwd_prof[i], (unsigned long long)ft[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2580,6 +2624,19 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdWaves - 1) / kFwdWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdWaves), 0, s, k);
+#if HN_PROFILE
+  {
+    unsigned long long f[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_fwd_prof), sizeof(f));
+    const double w = f[7] ? (double)f[7] : 1.;
+    fprintf(stderr, "hn_fwd_profile cycles/wave: coarse encode %.0f mlp %.0f | sample %.0f | fine encode %.0f "
+            "mlp %.0f | composite %.0f | total %.0f\n", f[0] / w, f[1] / w, f[2] / w, f[3] / w, f[4] / w,
+            f[5] / w, f[6] / w);
+    memset(f, 0, sizeof(f));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_prof), f, sizeof(f));
+  }
+#endif
   return hip_status(hipGetLastError());
 }
 

@@ -357,3 +357,31 @@ def test_fused_table_step_with_tv_bitwise(hn, mode):
     HF.L.check_device_faults()
     assert torch.equal(mf_, mr) and torch.equal(vf, vr)
     assert torch.equal(pf, pr)
+
+
+@pytest.mark.parametrize("perturb", [True, False])
+def test_fine_z_sort_structure(hn, perturb):
+    """sort(cat(z_vals, z_samples)) (run_nerf_helpers.py:551) in the forward
+    (merge_sort_z: bitonic importance run merged with the sorted coarse run):
+    every ray's fine z is non-decreasing, each coarse index appears exactly
+    once in fine_src at its own value, and the 128 others are tagged 255; on a
+    tie a coarse sample comes first (the rank sort's index order)."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, _ = _state(hn, 2048, 19, 23, "binned")
+    if not perturb:   # det sampling: u = linspace, many exact ties between the rays' samples
+        cfg = HF.make_render_cfg(emb.grid(), True, False, False, scatter="binned")
+        t_vals = torch.linspace(0., 1., 64, device=DEV)
+        u = torch.linspace(0., 1., 128, device=DEV).expand(2048, 128).contiguous()
+        _, st = HF.render_fwd(cfg, rays, t_vals, None, u, None, None, emb.table.detach(), ws, True)
+    zf, zc, src = st.z_f.cpu(), st.z_c.cpu(), st.fine_src.cpu().long()
+    assert (zf[:, 1:] >= zf[:, :-1]).all()
+    coarse = src < 64
+    assert (coarse.sum(1) == 64).all() and ((src == 255) | coarse).all()
+    pos = torch.full((zf.shape[0], 64), -1, dtype=torch.long)
+    rows = torch.arange(zf.shape[0])[:, None].expand_as(src)
+    pos[rows[coarse], src[coarse]] = torch.arange(192).expand_as(src)[coarse]
+    assert (pos >= 0).all()
+    assert torch.equal(torch.gather(zf, 1, pos), zc)
+    # coarse first on ties: no importance sample equal to a coarse value sits before it
+    prev = torch.cat([torch.full((zf.shape[0], 1), -1.0), zf[:, :-1]], 1)
+    prev_tag = torch.cat([torch.zeros((zf.shape[0], 1), dtype=torch.long), src[:, :-1]], 1)
+    assert not ((prev == zf) & coarse & (prev_tag == 255)).any()

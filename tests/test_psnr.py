@@ -134,6 +134,14 @@ def test_psnr_parity_equal_iterations(hn, oracle):
     seed = int(os.environ.get("HN_PSNR_SEED", "0"))
     tail_frac = float(os.environ.get("HN_PSNR_TAIL", "0.2"))   # the statistic's window: the last 20 % of the run
     tr = Trainer(args, data, DEV, seed=seed)
+    # HN_PSNR_LR_SCALE (calibration only): the HIP side trains at a scaled
+    # learning rate -- a deliberate regression that shows what size of PSNR
+    # loss the gate below catches
+    lr_scale = float(os.environ.get("HN_PSNR_LR_SCALE", "1"))
+    ref_lrate = args.lrate
+    tr.args.lrate = ref_lrate * lr_scale        # (tr.args is args)
+    for g in tr.optimizer.param_groups:
+        g["lr"] *= lr_scale
     box = tuple(torch.as_tensor(t, dtype=torch.float32).to(DEV) for t in data.bounding_box)
     res = O.level_resolutions(16, 16, args.finest_res)
     T = args.log2_hashmap_size
@@ -155,7 +163,7 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         cache = {c["iter"]: c["psnr_ref"] for c in cache["curve"]}
     curve = []
     t_hip = t_ref = 0.0
-    lr = args.lrate
+    lr = lr0 = ref_lrate                       # the reference path's own lr
     for i in range(1, iters + 1):                  # the reference loop's index (run_nerf.py:538-541)
         batch = tr.draw_batch(i)
         torch.cuda.synchronize()
@@ -168,8 +176,8 @@ def test_psnr_parity_equal_iterations(hn, oracle):
         torch.cuda.synchronize()
         t_hip += t1 - t0
         t_ref += time.perf_counter() - t1
-        lr = args.lrate * (0.1 ** ((i - 1) / (args.lrate_decay * 1000)))   # run_nerf.py:647-651
-        assert abs(lr - tr.optimizer.param_groups[0]["lr"]) <= 1e-12 * max(lr, 1.0)
+        lr = lr0 * (0.1 ** ((i - 1) / (args.lrate_decay * 1000)))   # run_nerf.py:647-651
+        assert abs(lr * lr_scale - tr.optimizer.param_groups[0]["lr"]) <= 1e-12 * max(lr, 1.0)
         if (i % every == 0 and (i > (1. - tail_frac) * iters or i % (5 * every) == 0)) or i == iters:
             ph, _ = _eval_hip(hn, tr, data)
             pr = cache[i] if cache is not None else _eval_oracle(O, ref, data, box, res, T)[0]
