@@ -212,39 +212,6 @@ HN_DEV void encode_level_off(const float* __restrict__ table, uint32_t lvl_row0,
   f0 = trilerp(e0, v.w);
   f1 = trilerp(e1, v.w);
 }
-// The same gathers by x-pairs: corners c and c + 4 (x0 and x0 + 1, the x
-// prime is 1) hash to rows h and h ^ 1 when x0 is even, i.e. one aligned
-// 16-byte pair of rows.  So each x-pair is one dwordx4 load of the pair that
-// holds h(x0), plus -- on the lanes whose x0 is odd only -- a dwordx2 load of
-// h(x0 + 1): 4 + 4 load instructions as before, a quarter fewer row requests.
-// Same values, same trilerp: bitwise
-// encode_level_off.  (x0 is odd exactly when h(x0 + 1) != h(x0) ^ 1: x0 + 1
-// then flips bit 1 too, which the mask keeps.)
-HN_DEV void encode_level_xpair(const float* __restrict__ table, uint32_t lvl_row0, const Voxel& v, float& f0,
-                               float& f1) {
-  float e0[8], e1[8];
-  const bool odd = v.h[4] != (v.h[0] ^ 1u);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const uint32_t r = lvl_row0 + v.h[c];
-    const f32x4 q = *reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(table) + (r & ~1u) * 8u);
-    const bool hi = (r & 1u) != 0u;
-    e0[c] = hi ? q.z : q.x;
-    e1[c] = hi ? q.w : q.y;
-    e0[c + 4] = hi ? q.x : q.z;   // even x0: h(x0 + 1) = h(x0) ^ 1
-    e1[c + 4] = hi ? q.y : q.w;
-  }
-  if (odd) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float2 t = ld_row(table, (lvl_row0 + v.h[c + 4]) * 8u);
-      e0[c + 4] = t.x;
-      e1[c + 4] = t.y;
-    }
-  }
-  f0 = trilerp(e0, v.w);
-  f1 = trilerp(e1, v.w);
-}
 HN_DEV void atomic_add_row(float* table, uint32_t byte_off, float g0, float g1) {
   float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(table) + byte_off);
   atomic_add_f32(p, g0);
