@@ -79,11 +79,23 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 // next chunk's during the current one's MFMAs measured 0.324 against 0.314 ms
 // for render_fwd_kernel, identical results).  f32: one group ahead.  The
 // scheduling barrier stops hipcc from hoisting all loads (register blowup).
+// Where a GEMM's packed A fragments come from (the packed buffer in global
+// memory: frag_load).
+struct FragGlobal {
+  const float* P;
+  HN_DEV f32x4 operator()(int off, int lane) const { return frag_load(P, off, lane); }
+};
+template <int R, typename BF, typename Src>
+HN_DEV f32x16 gemm_src(const Src& src, int ob, f32x16 acc, int lane, BF bval);
 template <int R, typename BF>
 HN_DEV f32x16 gemm(const float* __restrict__ P, int ob, f32x16 acc, int lane, BF bval) {
+  return gemm_src<R>(FragGlobal{P}, ob, acc, lane, bval);
+}
+template <int R, typename BF, typename Src>
+HN_DEV f32x16 gemm_src(const Src& src, int ob, f32x16 acc, int lane, BF bval) {
   constexpr int KS = kRegKS[R], NS = reg_ns(R), GPO = reg_gpo(R), OFF = reg_off(R);
-  // fragment group g of this block: frag_load (scalar offsets, hn_common.h)
-  auto ld = [&](int g) { return frag_load(P, OFF + (ob * GPO + g) * 256, lane); };
+  // fragment group g of this block (frag_load: scalar offsets, hn_common.h)
+  auto ld = [&](int g) { return src(OFF + (ob * GPO + g) * 256, lane); };
   if constexpr (NS > 0) {        // split-f32, fragments loaded at use
 #pragma unroll
     for (int c = 0; c < KS / 8; ++c) {
@@ -149,9 +161,17 @@ HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 
 // activation live until then -- that spilled the render forward 39 -> 158).
 // C0Init(ob): color_net.0's SH half for output block ob (constant along a ray:
 // the fused forward computes it once per ray and seeds every tile with it).
+template <bool MASKS = false, typename C0Init, typename Src>
+HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, MlpAct& a, f32x16& c2,
+                             int lane);
 template <bool MASKS = false, typename C0Init>
 HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0Init&& c0init,
                             MlpAct& a, f32x16& c2, int lane) {
+  mlp_fwd_tile_src<MASKS>(FragGlobal{P}, feat, c0init, a, c2, lane);
+}
+template <bool MASKS, typename C0Init, typename Src>
+HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, MlpAct& a, f32x16& c2,
+                             int lane) {
   a.m[0] = a.m[1] = a.m[2] = 0u;
   // sigma_net.0: 32 -> 64, ReLU
   // (Both output blocks of a GEMM sharing one B split per chunk, as the
@@ -159,18 +179,18 @@ HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0I
   // 0.307 ms, more spills at 4 waves per SIMD; r04c.)
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    a.h0[ob] = gemm<R_F0>(P, ob, zero16(), lane, [&](int s) { return feat[s]; });
+    a.h0[ob] = gemm_src<R_F0>(P, ob, zero16(), lane, [&](int s) { return feat[s]; });
     relu16(a.h0[ob]);
     if constexpr (MASKS) relu_mask_or(a.h0[ob], a.m[0], ob);
   }
   if constexpr (MASKS) asm volatile("" : "+v"(a.m[0]));
   // sigma_net.1: 64 -> 16 (sigma, geo15), no activation
-  a.s1 = gemm<R_F1>(P, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
+  a.s1 = gemm_src<R_F1>(P, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
   // color_net.0: [sh16 | geo15] -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
     f32x16 acc = c0init(ob);
-    acc = gemm<R_F2G>(P, ob, acc, lane, [&](int s) { return a.s1[s]; });
+    acc = gemm_src<R_F2G>(P, ob, acc, lane, [&](int s) { return a.s1[s]; });
     relu16(acc);
     if constexpr (MASKS) relu_mask_or(acc, a.m[1], ob);
     a.c0[ob] = acc;
@@ -179,13 +199,13 @@ HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0I
   // color_net.1: 64 -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    a.c1[ob] = gemm<R_F3>(P, ob, zero16(), lane, [&](int s) { return a.c0[s >> 4][s & 15]; });
+    a.c1[ob] = gemm_src<R_F3>(P, ob, zero16(), lane, [&](int s) { return a.c0[s >> 4][s & 15]; });
     relu16(a.c1[ob]);
     if constexpr (MASKS) relu_mask_or(a.c1[ob], a.m[2], ob);
   }
   if constexpr (MASKS) asm volatile("" : "+v"(a.m[2]));
   // color_net.2: 64 -> 3, no activation
-  c2 = gemm<R_F4>(P, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });
+  c2 = gemm_src<R_F4>(P, 0, zero16(), lane, [&](int s) { return a.c1[s >> 4][s & 15]; });
 }
 template <bool MASKS = false>
 HN_DEV void mlp_fwd_tile(const float* __restrict__ P, const f32x16& feat, const float sh8[8],

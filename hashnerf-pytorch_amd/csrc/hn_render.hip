@@ -230,20 +230,31 @@ __device__ unsigned long long g_fwd_prof[8];
 #define HN_FT_FEAT(i, f) ((void)0)
 #endif
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
+// (Round 4 measured 16-wave workgroups with each net's forward weight
+// fragments staged in LDS instead of streamed from L2 per tile: the MLP phase
+// ran ~3x faster but the gathers of 16 waves in step ~2.3x slower,
+// render_fwd_kernel 0.294 vs 0.281 ms, and staggering half of the waves made it
+// 0.301-0.313 ms; profiles/r04/r04e, r04f.)
+constexpr int kFwdBlockWaves = kFwdWaves;
+
+__global__ __launch_bounds__(64 * kFwdBlockWaves)
+__attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
 void render_fwd_kernel(RenderK k) {
-  __shared__ __attribute__((aligned(16))) float smem[kFwdWaves * kFLds + kGsLds];
-  const int wave = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) float smem[kFwdBlockWaves * kFLds + kGsLds];
+  // the wave index (and with it the ray, its 11 floats and every per-ray
+  // address) on the scalar unit: VGPR spills 45 -> 22, render_fwd_kernel
+  // 0.296 -> 0.281 ms (r04e)
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int p = lane & 31, h = lane >> 5;
-  float* gsl = smem + kFwdWaves * kFLds;
+  float* gsl = smem + kFwdBlockWaves * kFLds;
   stage_grid_sizes(k.g, gsl);
   __syncthreads();
   // XCD-aware: workgroup b runs on XCD b % 8, so consecutive ray groups of a
   // spatially ordered batch go to one XCD and share its L2
   const int64_t nb = gridDim.x;
   const int64_t grp = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
-  const int64_t ray = grp * kFwdWaves + wave;
+  const int64_t ray = grp * kFwdBlockWaves + wave;
   if (ray >= k.B) return;
 #if HN_PROFILE
   uint64_t ft[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -260,6 +271,8 @@ void render_fwd_kernel(RenderK k) {
   float* cdf = L + kFCdf;
   Ray r;
   load_ray(k.rays, ray, r);
+  float sh8[8], shx8[8];
+  float* c0l = L + kFC0;
 
   // ---- coarse z_vals (:514-536) ----
   auto zlin = [&](int i) {
@@ -278,12 +291,10 @@ void render_fwd_kernel(RenderK k) {
   zc[lane] = z;
   zsrc[lane] = z;
   k.z_coarse[ray * kSc + lane] = z;
-  float sh8[8], shx8[8];
   ray_sh(r, h, sh8, shx8);
   lds_fence_wave();
 
   // ---- coarse network (:540) ----
-  float* c0l = L + kFC0;
   c0sh_lds_store(opaque_ptr(k.Pc), sh8, c0l, lane);
   lds_fence_wave();
   for (int tau = 0; tau < kSc / 32; ++tau) {
@@ -2622,8 +2633,8 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.rgb0 = a->rgb0; k.depth0 = a->depth0; k.acc0 = a->acc0; k.sparsity0 = a->sparsity0;
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
-  const unsigned blocks = (unsigned)((a->n_rays + kFwdWaves - 1) / kFwdWaves);
-  hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdWaves), 0, s, k);
+  const unsigned blocks = (unsigned)((a->n_rays + kFwdBlockWaves - 1) / kFwdBlockWaves);
+  hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdBlockWaves), 0, s, k);
 #if HN_PROFILE
   {
     unsigned long long f[8];

@@ -1,7 +1,6 @@
 #!/bin/bash
-# Configs 3 and 5 made measurable like config 2 (PMC traffic + MFMA busy,
-# rocprofv3 kernel stats, bench lines with the CPU baseline at the config's B),
-# configs[3]'s per-rank shape on one GPU, and a 4-rank gloo rehearsal of configs[4].
+# MFMA hazard probes; configs 3 and 5 made measurable like config 2: PMC
+# traffic + MFMA busy and rocprofv3 kernel stats.
 set -o pipefail
 OUT=gpurun_out/r04d; mkdir -p $OUT
 export TMPDIR=/tmp
@@ -18,10 +17,3 @@ for C in 3 5; do
   python3 scripts/trace_tail_stats.py $(find $OUT/prof_c$C -name "*kernel_trace.csv" | head -1) 10 > $OUT/kernel_stats_config${C}_r04d.csv && rm -rf $OUT/prof_c$C
   head -8 $OUT/kernel_stats_config${C}_r04d.csv | cut -d, -f1-4
 done
-for C in 3 5 4; do
-  timeout -k 10 600 python bench.py --config $C > $OUT/bench_config${C}_r04d.json 2> $OUT/bench_config${C}_r04d.err || { echo "bench $C failed"; tail -3 $OUT/bench_config${C}_r04d.err; exit 1; }
-  python -c "import json;d=json.load(open('$OUT/bench_config${C}_r04d.json'));print($C, d['value'], d['ms_per_step'], d['roofline']['traffic'], d.get('cpu_baseline',{}).get('value'))"
-done
-timeout -k 10 600 python bench.py --gpus 4 --backend gloo --config 5 --steps 5 --warmup 2 --pretrain 20 --no-cpu-baseline \
-    > $OUT/bench_gloo4_config5_r04d.json 2> $OUT/bench_gloo4_config5_r04d.err || { echo "gloo4 failed"; tail -5 $OUT/bench_gloo4_config5_r04d.err; exit 1; }
-cat $OUT/bench_gloo4_config5_r04d.json | cut -c1-300
