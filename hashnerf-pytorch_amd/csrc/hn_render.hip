@@ -1426,7 +1426,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __shared__ uint32_t lovf;
   __shared__ uint32_t lvmxl[16 * 64];
   for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) lvmxl[i] = 0u;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
+  // wave-uniform work-unit arithmetic (u, ray = u / 3, u % 3, act) on the scalar unit
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = lane_id();
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
   if (threadIdx.x < 16) lvmx[threadIdx.x] = 0.f;
   if (threadIdx.x == 0) lovf = 0u;
@@ -1942,7 +1943,7 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
 // point instead of each redoing the ray's scans.
 __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   __shared__ float lds[kFwdWaves][kSf * 5];
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0) {   // binned scatter: no overflow records yet (count, per bin, cursors)
     const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);

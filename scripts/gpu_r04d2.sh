@@ -5,6 +5,8 @@
 set -o pipefail
 OUT=gpurun_out/r04d; mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > $OUT/pytest_gpu_d2.log 2>&1; RC=$?
+tail -2 $OUT/pytest_gpu_d2.log; [ $RC -eq 0 ] || exit $RC
 for C in 3 5 4; do
   timeout -k 10 600 python bench.py --config $C > $OUT/bench_config${C}_r04d.json 2> $OUT/bench_config${C}_r04d.err || { echo "bench $C failed"; tail -3 $OUT/bench_config${C}_r04d.err; exit 1; }
   python -c "import json;d=json.load(open('$OUT/bench_config${C}_r04d.json'));print($C, d['value'], d['ms_per_step'], d['roofline']['traffic'], d.get('cpu_baseline',{}).get('value'))"
