@@ -25,6 +25,10 @@
 
 #include <type_traits>
 
+#ifndef HN_XPAIR   // 1: the forward's gathers by x-pairs (encode_level_xpair), 0: 8 row loads per level
+#define HN_XPAIR 0
+#endif
+
 namespace hn {
 
 constexpr int kSc = 64, kNi = 128, kSf = 192;
@@ -166,6 +170,9 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
 #pragma unroll
   for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], g.bmin[a], g.bmax[a]);
   const uint32_t mask = (1u << g.log2T) - 1u;
+#if HN_XPAIR
+  const __amdgpu_buffer_rsrc_t rs = table_rsrc(table, (uint32_t)g.n_levels << (g.log2T + 3));
+#endif
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     const int l0 = tile_level(m, 0), l1 = tile_level(m, 1);
@@ -175,10 +182,22 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     Voxel v;
     voxel_level_rcp(pt, xc, gs, rg, g.bmin, mask, v);
     float f0, f1;
+#if HN_XPAIR
+    encode_level_xpair(rs, l << g.log2T, v, f0, f1);
+    asm volatile("" : "+v"(f0), "+v"(f1));   // the level's interpolation here: its 24 data registers die
+#else
     encode_level_off(table, l << g.log2T, v, f0, f1);
+#endif
     feat[2 * m] = f0;
     feat[2 * m + 1] = f1;
+#if HN_XPAIR
+    // one level's 4 + 4 loads in flight (24 data registers); the memory clobber
+    // keeps the next level's buffer loads below this level's use
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#else
     if (m & 1) __builtin_amdgcn_sched_barrier(0);   // <= 16 gathers in flight
+#endif
   }
 }
 
@@ -345,8 +364,8 @@ void render_fwd_kernel(RenderK k) {
   // the bitonic-sorted importance samples (rawb is free until the fine tiles),
   // the all-pairs rank sort if the coarse run is ever out of order
   // (render_fwd_kernel 0.2998 -> 0.2966 ms, r04c)
-  if (!merge_sort_z(zsrc, zs, rawb, lane, k.fine_src + ray * kSf))
-    rank_sort_wave(zsrc, zs, kSf, lane, k.fine_src + ray * kSf, kSc);
+  uint8_t* org = k.fine_src + ray * kSf;
+  if (!merge_sort_z(zsrc, zs, rawb, lane, org)) rank_sort_wave(zsrc, zs, kSf, lane, org, kSc);
   for (int i = lane; i < kSf; i += 64) k.z_fine[ray * kSf + i] = zs[i];
 
   // ---- fine network (:556) ----
@@ -359,7 +378,26 @@ void render_fwd_kernel(RenderK k) {
     float pt[3];
     ray_point(r, zs[q], pt);
     f32x16 feat;
-    encode_tile(k.g, gsl, k.table, pt, h, feat);
+    // a third of the fine samples are the coarse samples again (the merge
+    // keeps their z bitwise): with the feature cache present, those lanes load
+    // the coarse tile's features (4 dwordx4, written by this wave) instead of
+    // gathering 16 levels x 8 corners again -- a quarter of the ray's gathers
+    // (render_fwd_kernel 0.282 -> 0.275 ms, r04h).  Encoding only the 128
+    // importance samples as 4 full tiles first and loading every fine tile's
+    // features back from the cache (a third fewer encode instructions) measured
+    // slower: 0.301 ms, the waves then run their MLP tiles in step (r04j).
+    const int src = k.feat ? (int)k.fine_src[ray * kSf + q] : 255;
+    if (src >= kSc) {
+      encode_tile(k.g, gsl, k.table, pt, h, feat);
+    } else {
+      const f32x4* t = reinterpret_cast<const f32x4*>(k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY +
+                                                      (size_t)(src >> 5) * 1024) + (src & 31) + 32 * h;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f32x4 v = t[64 * c];
+        feat[4 * c] = v.x; feat[4 * c + 1] = v.y; feat[4 * c + 2] = v.z; feat[4 * c + 3] = v.w;
+      }
+    }
     HN_FT_FEAT(3, feat);
     if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
     MlpAct a;

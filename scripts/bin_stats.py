@@ -22,6 +22,8 @@ def bin_geom(T, n):
     rpb = (n + BLOCKS - 1) // BLOCKS
     avg = rpb * 192 * 4 * 2.0 ** (shift - T)
     cap = (int(avg) + 128 + 63) & ~63
+    if ((cap >> 6) & 1) == 0:   # an odd multiple of 64 (hn_render.hip bin_geom)
+        cap += 64
     return shift, nbins, cap
 
 
@@ -32,6 +34,7 @@ def main():
     ap.add_argument("--log2T", type=int, default=19)
     ap.add_argument("--finest", type=int, default=512)
     ap.add_argument("--quick", action="store_true", help="counts only (no owner / precision study)")
+    ap.add_argument("--dups", action="store_true", help="records vs distinct entries per region / bin, per level")
     a = ap.parse_args()
     import hn_loader
     hn_loader.load()
@@ -76,6 +79,31 @@ def main():
         print("max region fill per level:", " ".join(str(int(x)) for x in mx))
         spill = np.maximum(cnt - cap, 0).sum(1).reshape(-1, bins_per_level).sum(1)
         print("spilled records per level:", " ".join(str(int(x)) for x in spill))
+    if a.dups:
+        # merge potential: per level, records vs distinct entry words inside
+        # one producer's region of a bin (what an in-block merge could fold),
+        # and inside a whole bin over all producers (the owner's view)
+        idx_i = off + 4 * nrec
+        wr = ws[idx_i: idx_i + nbins * BLOCKS * cap].view(nbins, BLOCKS, cap).to(torch.int64) & 0xffffffff
+        cm = torch.from_numpy(np.minimum(cnt, cap)).to(wr.device)
+        valid = torch.arange(cap, device=wr.device)[None, None, :] < cm[:, :, None]
+        big = torch.iinfo(torch.int64).max
+        srt, _ = torch.sort(torch.where(valid, wr, big), dim=2)
+        newv = torch.ones_like(srt, dtype=torch.bool)
+        newv[:, :, 1:] = srt[:, :, 1:] != srt[:, :, :-1]
+        dist_region = ((newv & (srt != big)).sum(2)).sum(1).cpu().numpy()      # per bin
+        flat = torch.where(valid, wr, big).reshape(nbins, -1)
+        sb, _ = torch.sort(flat, dim=1)
+        nb_ = torch.ones_like(sb, dtype=torch.bool)
+        nb_[:, 1:] = sb[:, 1:] != sb[:, :-1]
+        dist_bin = (nb_ & (sb != big)).sum(1).cpu().numpy()
+        recs = np.minimum(cnt, cap).sum(1)
+        per = lambda x: x.reshape(-1, bins_per_level).sum(1)
+        print("level: records (in regions) / distinct per producer region / distinct per bin")
+        for l, (r_, d1, d2) in enumerate(zip(per(recs), per(dist_region), per(dist_bin))):
+            print(f"  {l:2d}: {int(r_):9d} {int(d1):9d} ({r_ / max(d1, 1):.2f}x) {int(d2):9d} ({r_ / max(d2, 1):.2f}x)")
+        print(f"  all: {int(recs.sum())} {int(dist_region.sum())} ({recs.sum() / dist_region.sum():.2f}x) "
+              f"{int(dist_bin.sum())} ({recs.sum() / dist_bin.sum():.2f}x)")
     if a.quick:
         HF.L.check_device_faults()
         return
