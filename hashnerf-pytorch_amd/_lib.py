@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 11                # HN_ABI_VERSION
+ABI_VERSION = 12                # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 9728      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -42,7 +42,7 @@ class HnMlpGrad(C.Structure):
 class HnRenderCfg(C.Structure):
     _fields_ = [("grid", HnGrid), ("n_samples", C.c_int32), ("n_importance", C.c_int32),
                 ("white_bkgd", C.c_int32), ("lindisp", C.c_int32), ("perturb", C.c_int32),
-                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("reserved", C.c_int32)]
+                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("merge_levels", C.c_int32)]
 
 
 _P = C.c_void_p
@@ -73,7 +73,7 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
                 ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
-                ("table_live", _P), ("table_live_levels", C.c_int32), ("reserved", C.c_int32)]
+                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32)]
 
 
 class HnTvArgs(C.Structure):
@@ -135,6 +135,9 @@ SIGNATURES = {
                                   C.c_size_t, _P]),
     "hn_render_bwd": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderBwdArgs), _P,
                                   C.c_size_t, _P]),
+    "hn_render_bins": (C.c_int32, [C.POINTER(HnRenderCfg), C.c_int64, C.POINTER(C.c_int32)]),
+    "hn_render_bwd_owner": (C.c_int32, [C.POINTER(HnRenderCfg), C.POINTER(HnRenderBwdArgs), _P,
+                                        C.c_size_t, C.c_int32, C.c_int32, _P]),
 }
 
 

@@ -1275,6 +1275,18 @@ HN_DEV void seg_sum4(float (&v)[4], uint32_t pm, int pp, bool s1, bool s2, bool 
   }
 }
 
+// round(v * 2^S) as int64 without f64 arithmetic: x = v * 2^S is exact in fp32
+// (|x| < 2^47, a power-of-2 scale), a = trunc(x / 2^16) is an exact integer
+// (|a| < 2^31),
+// b = x - a * 2^16 exact with |b| < 2^16, and round(x) = a * 2^16 + rint(b)
+// (ties to even agree: a * 2^16 is even).
+HN_DEV long long fx_of(float v, float scale) {
+  const float x = v * scale;
+  const float a = truncf(x * 0x1p-16f);
+  const float b = __builtin_fmaf(-a, 0x1p16f, x);
+  return ((long long)(int32_t)a << 16) + (long long)(int32_t)rintf(b);
+}
+
 // A run head's record: the x-pair (x0 = cx, x1 = cx + 1) of corner row (yy, zz)
 // (the y / z coordinates times their primes) at level l.  rec_slot takes the
 // record's slot in its bin (LDS counter); rec_store writes it -- split so a
@@ -1420,6 +1432,7 @@ struct ScK {
   const float* slab;       // NULL: no slab reduction here
   hn_mlp_grad dc, df;
   int32_t overwrite_mlp;
+  int32_t merge_levels;    // levels 0 .. merge_levels-1: records merged per block (merge table)
 };
 constexpr int kScWaves = 16;
 constexpr int kScMaxBinsLog2 = 13;
@@ -1445,6 +1458,11 @@ constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per 
 // wave cycles), not on the write traffic.
 constexpr int kStLog2 = 12, kStPool = 1 << kStLog2;   // 64 KiB of values + 16 KiB of words
 constexpr int kStMinLog2C = 3;                          // fewer than 8 records per bin: no staging
+// Merge table of the coarse levels (over the pool's LDS): entry words and
+// their 4 sums as 64-bit fixed point, 36 B per slot
+constexpr int kMhSlotsLog2 = 11, kMhSlots = 1 << kMhSlotsLog2;
+constexpr uint32_t kMhEmpty = 0xffffffffu;   // never an entry word (bits 26-27 are zero)
+static_assert(kMhSlots * 36 <= kStPool * 20, "the merge table fits the staging pool");
 struct StPhase {
   int b0, log2c;   // first bin of the level, log2 pool records per bin (< kStMinLog2C: direct)
   int nbl;         // bins of the level
@@ -1491,15 +1509,24 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int64_t u0 = (int64_t)blockIdx.x * per;
   const int64_t u1 = u0 + per < units ? u0 + per : units;
   const int pp = lane & 15;
-  __shared__ f32x4 stv[kStPool];
-  __shared__ uint32_t stw[kStPool];
+  // the staging pool (fine levels) and, over the same LDS, the merge table
+  // (merged levels): 80 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t st_raw[kStPool * 5];
+  f32x4* const stv = reinterpret_cast<f32x4*>(st_raw);
+  uint32_t* const stw = st_raw + 4 * kStPool;
+  uint32_t* const mh_w = st_raw;                                                      // [kMhSlots] words
+  unsigned long long* const mh_v = reinterpret_cast<unsigned long long*>(st_raw + kMhSlots);   // [4][kMhSlots]
   __shared__ uint32_t stfl[2][kStPool >> kStMinLog2C];   // per phase parity: first staged slot per bin
+  __shared__ uint32_t mh_bound[16], mh_fail;
   const int log2T = (int)k.g.log2T, sh = k.bin_shift;
+  const int n_merge = k.merge_levels;
   // first staged slot of each bin of level l (the bins' counts so far, capped)
-  auto st_init = [&](int l) {
+  // (stfl alternates between phases: par = the phase's parity)
+  int par = 0;
+  auto st_init = [&](int l, int pr) {
     const StPhase ph = st_phase(l, log2T, sh);
     if (ph.log2c < kStMinLog2C) return;
-    for (int i = threadIdx.x; i < ph.nbl; i += blockDim.x) stfl[l & 1][i] = min(bcnt[ph.b0 + i], bw.cap);
+    for (int i = threadIdx.x; i < ph.nbl; i += blockDim.x) stfl[pr][i] = min(bcnt[ph.b0 + i], bw.cap);
   };
   // the pool's records of level l to their regions, in slot order
   auto st_flush = [&](int l) {
@@ -1508,7 +1535,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     const uint32_t c = 1u << ph.log2c;
     for (int p = threadIdx.x; p < kStPool; p += blockDim.x) {
       const int bl = p >> ph.log2c, b = ph.b0 + bl;
-      const uint32_t j = (uint32_t)p & (c - 1u), f = stfl[l & 1][bl];
+      const uint32_t j = (uint32_t)p & (c - 1u), f = stfl[par][bl];
       const uint32_t end = min(min(bcnt[b], bw.cap), f + c);
       if (f + j < end) {
         const size_t r = bw.base + (size_t)b * bw.stride + f + j;
@@ -1517,109 +1544,232 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       }
     }
   };
-  st_init(0);
-  __syncthreads();
+  // the merge table empty (every merged level leaves it empty again)
+  auto mh_clear = [&]() {
+    for (int s = threadIdx.x; s < kMhSlots; s += blockDim.x) {
+      mh_w[s] = kMhEmpty;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) mh_v[c * kMhSlots + s] = 0ull;
+    }
+  };
   const int64_t n_it = (u1 - u0 + kScWaves - 1) / kScWaves;   // the same for every wave of the block
-  [[maybe_unused]] constexpr int g = 0;
-  for (int64_t it = 0; it < n_it; ++it) {
-    const int64_t u = u0 + wave + it * kScWaves;
-    const bool act = u < u1;
-    const int64_t ray = u / 3;
-    const int i = 64 * (int)(u % 3) + lane;       // fine sample
+  // one unit's inputs: its ray, point and (fine + coarse twin) grads of one level
+  struct Unit {
+    bool act;
     Ray r;
     float pt[3], xc[3];
-    // one level of the unit: voxel, run heads, the 4 corner rows' records
-    auto level = [&](const int l, const float g0, const float g1) {
-        const StPhase ph = st_phase(l, log2T, sh);
-        const bool staged = ph.log2c >= kStMinLog2C;
-        if (act) {
-        int32_t cell[3];
-        float w[3];
-        voxel_cw_sc(k.g, gsl, pt, xc, l, cell, w);
-        const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
-        const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
-        const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
-        const uint64_t hb = __ballot(head);
-        const uint32_t pm = (uint32_t)(hb >> (lane & 48)) & 0xffffu;
-        // lane 0 of every row is a head, so these never carry across rows
-        const uint64_t nz1 = ~hb & 0xfffefffefffefffeull, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
-        const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
-      
-        const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
-        // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
-        const float gz[2][2] = {{g0 * az, g1 * az}, {g0 * w[2], g1 * w[2]}};   // [k][f]
-        float vmax = 0.f;   // largest |record value| of the level: the owner's fixed-point scale
-        float v[4][4];
-        RecSlot rs[4];
+    float g0, g1;
+  };
+  bool bad = false;   // a non-finite grad or point seen by this lane
+  auto unit_at = [&](int64_t it, int l) {
+    Unit q;
+    const int64_t u = u0 + wave + it * kScWaves;
+    q.act = u < u1;
+    q.g0 = q.g1 = 0.f;
+    if (q.act) {
+      const int64_t ray = u / 3;
+      const int i = 64 * (int)(u % 3) + lane;       // fine sample
+      load_ray(k.rays, ray, q.r);
+      ray_point(q.r, k.z_fine[ray * kSf + i], q.pt);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {   // sums and slots of the 4 corner rows: 4 counter round trips in flight
+      for (int a = 0; a < 3; ++a) q.xc[a] = clamp_t(q.pt[a], k.g.bmin[a], k.g.bmax[a]);
+      // level l = element 2 (l & 1) .. of level pair l / 2 (tile_level: chunk
+      // lp / 2 of lane half lp % 2)
+      const int lp = l >> 1, e = 2 * (l & 1);
+      const float* tb = k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024 +
+                        4 * (64 * (lp >> 1) + 32 * (lp & 1) + (i & 31)) + e;
+      float2 gq = *reinterpret_cast<const float2*>(tb);
+      const int src = k.fine_src[ray * kSf + i];
+      if (src < kSc) {                          // coarse twin: fine + coarse grads
+        const float2 t2 = *reinterpret_cast<const float2*>(
+            k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024 +
+            4 * (64 * (lp >> 1) + 32 * (lp & 1) + (src & 31)) + e);
+        gq = make_float2(gq.x + t2.x, gq.y + t2.y);
+      }
+      q.g0 = gq.x;
+      q.g1 = gq.y;
+      const float chk = (gq.x + gq.y) + (l == 0 ? (q.pt[0] + q.pt[1]) + q.pt[2] : 0.f);
+      bad |= !(fabsf(chk) <= 3.402823466e38f);
+    }
+    return q;
+  };
+  // The records of one level of a unit: voxel, run heads, per corner row the
+  // x-pair sums over runs of samples in one voxel (16-lane rows), then each
+  // head lane's record to sink(c, word, bin-relative slot source, v) per mode:
+  //   kStaged: the staging pool / direct store (slots from the LDS counters),
+  //   kDirect: direct store,
+  //   kMerged: the merge table (int64 at the level's block scale `mscale`)
+  enum { kStaged = 0, kDirect = 1, kMerged = 2 };
+  auto level = [&](const Unit& q, const int l, const int mode, const float mscale) {
+    if (!q.act) return;
+    const StPhase ph = st_phase(l, log2T, sh);
+    const bool staged = mode == kStaged && ph.log2c >= kStMinLog2C;
+    int32_t cell[3];
+    float w[3];
+    voxel_cw_sc(k.g, gsl, q.pt, q.xc, l, cell, w);
+    const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
+    const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
+    const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
+    const uint64_t hb = __ballot(head);
+    const uint32_t pm = (uint32_t)(hb >> (lane & 48)) & 0xffffu;
+    // lane 0 of every row is a head, so these never carry across rows
+    const uint64_t nz1 = ~hb & 0xfffefffefffefffeull, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
+    const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
+    const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
+    // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
+    const float gz[2][2] = {{q.g0 * az, q.g1 * az}, {q.g0 * w[2], q.g1 * w[2]}};   // [k][f]
+    float vmax = 0.f;   // largest |record value| of the level: the owner's fixed-point scale
+    float v[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int j = c >> 1, kk = c & 1;
+      const float wy = j ? w[1] : ay;
+      const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
+      v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
+      seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
+      vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+    }
+    if (mode == kMerged) {
+      if (head) {
+        bool fail = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
           const int j = c >> 1, kk = c & 1;
-          const float wy = j ? w[1] : ay;
-          const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
-          v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
-          seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
-          vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
-          if (head) rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)k.g.log2T, cx, j ? y0 + kPrimeY : y0,
-                                     kk ? z0 + kPrimeZ : z0);
-        }
-        if (head) {
+          const uint32_t yy = j ? y0 + kPrimeY : y0, zz = kk ? z0 + kPrimeZ : z0;
+          const uint32_t flat = ((uint32_t)l << log2T) + ((cx ^ yy ^ zz) & ((1u << log2T) - 1u));
+          const uint32_t word = flat | (((uint32_t)__builtin_ctz(~cx) + 1u) << 28);
+          // every value must convert exactly (|v * scale| < 2^46): else the
+          // level is redone unmerged
+          bool ok = true;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[l & 1][staged ? bl : 0];
-            if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
-              const int q = (int)((bl << ph.log2c) + j);
-              stv[q] = f32x4{v[c][0], v[c][1], v[c][2], v[c][3]};
-              stw[q] = rs[c].word;
-              continue;
-            }
-            rec_store(bw, rs[c], v[c]);
+          for (int e = 0; e < 4; ++e) ok = ok && fabsf(v[c][e] * mscale) < 0x1p46f;
+          uint32_t s = (word * 0x9E3779B1u) >> (32 - kMhSlotsLog2);
+          int probes = 0;
+          while (ok) {   // linear probing over the whole table: fails only when it is full
+            uint32_t cur = kMhEmpty;
+            __hip_atomic_compare_exchange_strong(mh_w + s, &cur, word, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur == kMhEmpty || cur == word) break;
+            s = (s + 1u) & (kMhSlots - 1u);
+            ok = ++probes < kMhSlots;
           }
+          if (!ok) {
+            fail = true;
+            continue;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __hip_atomic_fetch_add(mh_v + e * kMhSlots + s, (unsigned long long)fx_of(v[c][e], mscale),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (fail) mh_fail = 1u;
+      }
+      return;   // the flush reports the merged values' maximum
+    }
+    RecSlot rs[4];
+    if (head) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {   // 4 counter round trips in flight
+        const int j = c >> 1, kk = c & 1;
+        rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)log2T, cx, j ? y0 + kPrimeY : y0, kk ? z0 + kPrimeZ : z0);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[par][staged ? bl : 0];
+        if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
+          const int qq = (int)((bl << ph.log2c) + j);
+          stv[qq] = f32x4{v[c][0], v[c][1], v[c][2], v[c][3]};
+          stw[qq] = rs[c].word;
+          continue;
+        }
+        rec_store(bw, rs[c], v[c]);
+      }
+    }
+    __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  // Merged levels: the level's scale from a bound on its record values,
+  // 16 x the largest |grad| of the block's units (a run sums <= 16 samples of
+  // one row; trilinear weights are <= 1 inside the box, and a value past the
+  // bound's 2^6 margin sends the level to the unmerged path)
+  if (n_merge > 0) {
+    if (threadIdx.x < 16) mh_bound[threadIdx.x] = 0u;
+    mh_clear();
+    if (threadIdx.x == 0) mh_fail = 0u;
+    __syncthreads();
+    for (int l = 0; l < n_merge; ++l) {
+      float m = 0.f;
+      for (int64_t it = 0; it < n_it; ++it) {
+        const Unit q = unit_at(it, l);
+        m = fmaxf(m, fmaxf(fabsf(q.g0), fabsf(q.g1)));
+      }
+      m = wave_max_f32(m);
+      if (lane == 0)
+        __hip_atomic_fetch_max(mh_bound + l, __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  if (n_merge < 16) st_init(n_merge, par);
+  __syncthreads();
+  for (int l = 0; l < 16; ++l) {
+    if (l < n_merge) {
+      // scale 2^S: values < 2^(E_B) -> < 2^40 units, E_B the exponent of the bound
+      const float bnd = 16.f * __uint_as_float(mh_bound[l]);
+      const int eb = bnd > 0.f && bnd <= 3.0e38f ? ilogbf(bnd) + 1 : 0;
+      const int S0 = 40 - eb;
+      const int S = S0 > 127 ? 127 : (S0 < -126 ? -126 : S0);
+      const float mscale = ldexpf(1.f, S);
+      for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kMerged, mscale);
+      __syncthreads();   // the level's sums are complete
+      const bool failed = mh_fail != 0u;   // uniform
+      if (!failed) {
+        // one record per distinct entry word: the block's exact sum, rounded once to fp32
+        float vmax = 0.f;
+        for (int s = threadIdx.x; s < kMhSlots; s += blockDim.x) {
+          const uint32_t word = mh_w[s];
+          if (word == kMhEmpty) continue;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = ldexpf((float)(long long)mh_v[e * kMhSlots + s], -S);
+            mh_v[e * kMhSlots + s] = 0ull;
+            vmax = fmaxf(vmax, fabsf(v[e]));
+          }
+          mh_w[s] = kMhEmpty;
+          RecSlot rs;
+          rs.word = word;
+          rs.bin = (word & 0x0fffffffu) >> bw.shift;
+          rs.slot = __hip_atomic_fetch_add(bw.lcnt + rs.bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          rec_store(bw, rs, v);
         }
         __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
-        }   // act
-      __syncthreads();   // the phase's records are in the pool, its counts final
-      st_flush(l);
-      st_init(l + 1 < 16 ? l + 1 : 0);   // the next phase's bins (other parity), counts unchanged by the flush
-      __syncthreads();   // the pool is free again
-    };
-    // grads loaded per level pair inside a rolled loop (one copy of the level
-    // code for two levels instead of sixteen: the unrolled kernel was 84 KB,
-    // over the 64 KB instruction cache two CUs share)
-    const f32x4* tb = nullptr;
-    const f32x4* tw = nullptr;
-    int src = kSc;
-    float chk = 0.f;
-    if (act) {
-      load_ray(k.rays, ray, r);
-      ray_point(r, k.z_fine[ray * kSf + i], pt);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], k.g.bmin[a], k.g.bmax[a]);
-      tb = reinterpret_cast<const f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024);
-      src = k.fine_src[ray * kSf + i];
-      if (src < kSc) tw = reinterpret_cast<const f32x4*>(k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024);
-      chk = (pt[0] + pt[1]) + pt[2];
-    }
-    // level pair lp = levels 2 lp, 2 lp + 1 = chunk lp / 2 of lane half lp % 2
-    // (tile_level): elements (f0, f1) of the lower level, then of the upper
-#pragma clang loop unroll(disable)
-    for (int lp = 0; lp < 8; ++lp) {
-      f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (act) {
-        q = tb[64 * (lp >> 1) + 32 * (lp & 1) + (i & 31)];
-        if (src < kSc) {                          // coarse twin: fine + coarse grads
-          const f32x4 e = tw[64 * (lp >> 1) + 32 * (lp & 1) + (src & 31)];
-          q = f32x4{q.x + e.x, q.y + e.y, q.z + e.z, q.w + e.w};
-        }
-        chk += (q.x + q.y) + (q.z + q.w);
+      } else {
+        // the table overflowed (or a value exceeded the bound): this block
+        // writes the level's records unmerged (a function of the block's
+        // records alone, so the result stays deterministic)
+        __syncthreads();   // every lane has read mh_fail
+        mh_clear();
+        if (threadIdx.x == 0) mh_fail = 0u;
+        for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kDirect, 1.f);
       }
-      level(2 * lp, q.x, q.y);
-      level(2 * lp + 1, q.z, q.w);
+      if (l + 1 == n_merge && l + 1 < 16) st_init(l + 1, par);
+      __syncthreads();   // the table is empty again
+    } else {
+      for (int64_t it = 0; it < n_it; ++it) {
+        level(unit_at(it, l), l, kStaged, 1.f);
+        __syncthreads();   // the phase's records are in the pool, its counts final
+        st_flush(l);
+        // the next phase's bins (other parity), counts unchanged by the flush
+        const int ln = it + 1 < n_it ? l : l + 1;
+        if (ln < 16) st_init(ln, par ^ 1);
+        __syncthreads();   // the pool is free again
+        par ^= 1;
+      }
     }
-    // non-finite inputs (NaN / Inf in a grad or the point): one test per lane
-    if (act && __ballot(!(fabsf(chk) <= 3.402823466e38f)) != 0ull && lane == 0)
-      __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // non-finite inputs (NaN / Inf in a grad or the point): one test per lane
+  if (__ballot(bad) != 0ull && lane == 0)
+    __hip_atomic_fetch_or(&g_hn_fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (k.tv_off[16] > 0) {
     // The TV term's table gradient: one record per x-pair (x0, x0 + 1) of cube
     // vertices of one (y, z) row, d TV_l / d e (tv_grad) scaled by g_tv[l] /
@@ -1676,7 +1826,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
   if (k.slab) {   // the dW slabs are complete (the MLP-backward kernel ran before this one)
     float(*part)[64] = reinterpret_cast<float(*)[64]>(stv);   // the staging pool is free now
-    static_assert(sizeof(stv) >= sizeof(float) * kSlabGroups * 64 && 64 * kScWaves == 64 * kSlabGroups,
+    static_assert(sizeof(st_raw) >= sizeof(float) * kSlabGroups * 64 && 64 * kScWaves == 64 * kSlabGroups,
                   "slab-reduce blocks inside the scatter blocks");
     // the 292 slab blocks go to the scatter blocks as they finish (a counter
     // reset by render_comp_bwd_kernel): the sums do not depend on who runs them
@@ -2238,6 +2388,7 @@ struct BinR {
   hn_radam_tensor step;
   const uint32_t* live;    // fused step: live row pairs of levels < live_levels (hn_render_bwd_args.table_live)
   int32_t live_levels;
+  int32_t bin0;            // first bin of the launch (hn_render_bwd_owner ranges)
 };
 constexpr int kBinThreads = 1024;
 constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2^13 floats / 4 / 1024)
@@ -2253,16 +2404,6 @@ static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 en
 constexpr int kBrDepth = HN_BR_DEPTH;
 constexpr int kBrChunks = 8192;   // table entries (16 KiB of LDS): bins of up to 512 K records
 
-// round(v * 2^S) as int64 without f64 arithmetic: x = v * 2^S is exact in fp32
-// (|x| < 2^41, a power-of-2 scale), a = trunc(x / 2^16) is an exact integer,
-// b = x - a * 2^16 exact with |b| < 2^16, and round(x) = a * 2^16 + rint(b)
-// (ties to even agree: a * 2^16 is even).
-HN_DEV long long fx_of(float v, float scale) {
-  const float x = v * scale;
-  const float a = truncf(x * 0x1p-16f);
-  const float b = __builtin_fmaf(-a, 0x1p16f, x);
-  return ((long long)(int32_t)a << 16) + (long long)(int32_t)rintf(b);
-}
 
 // acc: [feature][entry] (entry e's accumulators 8 B apart per feature: a
 // wave's random entries spread over twice the LDS banks of [entry][feature])
@@ -2349,7 +2490,7 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __shared__ uint32_t wsum[kBwdBlocks / 64], wmax[kBwdBlocks / 64];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(acc4);
   const int n4 = (2 << k.shift) / 2;   // f32x4 = 2 accumulators
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = (uint32_t)k.bin0 + blockIdx.x;
   const size_t e0 = (size_t)b << (k.shift + 1);   // first float of the slice
   const int nd4 = (2 << k.shift) / 4;             // float4s of the slice (<= 4 per thread)
   // fused step on a coarse level: the row pairs no gradient can reach (their
@@ -2571,6 +2712,34 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
 // Backward schedule: cfg->scatter 1 = float atomics (fused), 2 = binned
 // (split), 0 = binned unless the environment sets HN_SCATTER=atomic.  The
 // binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 22).
+// Levels whose records the scatter merges per block (a prefix: the levels
+// of at most kMergeMaxCells cells per axis, where a block's 16 neighbouring
+// rays cross few distinct voxels; config 2: levels 0-9, 2.5-23x fewer records
+// per block, scripts/bin_stats.py --dups).  hn_render_cfg.merge_levels, or
+// HN_SC_MERGE_LEVELS=n when that is 0 (automatic), overrides.
+constexpr double kMergeMaxCells = 130.0;
+static int merge_levels(const hn_render_cfg* c) {
+  static const int env = [] {
+    const char* e = getenv("HN_SC_MERGE_LEVELS");
+    return e ? atoi(e) : -1;
+  }();
+  const hn_grid& g = c->grid;
+  const int want = c->merge_levels != 0 ? c->merge_levels : env;
+  if (want >= 0 || c->merge_levels < 0) return want < 0 ? 0 : (want < g.n_levels ? want : g.n_levels);
+  int n = 0;
+  for (int l = 0; l < g.n_levels; ++l) {
+    double cells = 0.0;
+    for (int a = 0; a < 3; ++a) {
+      const double gs = g.grid_size[l][a];
+      const double c = gs > 0.0 ? ((double)g.box_max[a] - g.box_min[a]) / gs : 1e30;
+      cells = c > cells ? c : cells;
+    }
+    if (cells > kMergeMaxCells) break;
+    n = l + 1;
+  }
+  return n;
+}
+
 static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   static int env = -1;
   if (env < 0) {
@@ -2690,6 +2859,55 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   return hip_status(hipGetLastError());
 }
 
+// The owner pass's arguments (bins [bin0, ...) of one launch)
+static BinR owner_args(const hn_render_cfg* cfg, const hn_render_bwd_args* a, float* bins, const BinGeom& bg,
+                       int bin0) {
+  BinR r;
+  r.bins = bins;
+  r.n_rays = a->n_rays;
+  r.nbins = bg.nbins;
+  r.cap = bg.cap;
+  r.shift = bg.shift;
+  r.log2T = cfg->grid.log2_hashmap_size;
+  r.d_table = a->d_table;
+  r.overwrite = (a->d_table_mode & 1) != 0;
+  r.fused = a->table_step != nullptr;
+  if (r.fused) r.step = *a->table_step;
+  r.live = r.fused ? a->table_live : nullptr;
+  r.live_levels = r.live ? a->table_live_levels : 0;
+  r.bin0 = bin0;
+  return r;
+}
+
+extern "C" int32_t hn_render_bins(const hn_render_cfg* cfg, int64_t n_rays, int32_t* shift) {
+  if (!cfg || !shift) return 0;
+  if (check_cfg(cfg) || bwd_mode(cfg, n_rays) != kModeSplit) {
+    *shift = 0;
+    return 0;
+  }
+  const BinGeom bg = bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap);
+  *shift = bg.shift;
+  return bg.nbins;
+}
+
+extern "C" int32_t hn_render_bwd_owner(const hn_render_cfg* cfg, const hn_render_bwd_args* a, void* workspace,
+                                       size_t ws_bytes, int32_t bin_lo, int32_t bin_hi, void* stream) {
+  int32_t st = check_cfg(cfg);
+  if (st) return st;
+  if (!a || !workspace) return HN_E_NULL;
+  if (!a->owner_defer || a->n_rays <= 0 || bwd_mode(cfg, a->n_rays) != kModeSplit) return HN_E_SHAPE;
+  if (!a->d_table && !a->table_step) return HN_E_NULL;
+  if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
+  const BinGeom bg = bin_geom(cfg->grid.log2_hashmap_size, a->n_rays, cfg->bin_cap);
+  if (bin_lo < 0 || bin_hi > bg.nbins || bin_lo > bin_hi) return HN_E_SHAPE;
+  if (bin_lo == bin_hi) return HN_OK;
+  const WsLayout wl = ws_layout(cfg, a->n_rays, kModeSplit);
+  const BinR r = owner_args(cfg, a, (float*)workspace + wl.bins, bg, bin_lo);
+  hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)(bin_hi - bin_lo)), dim3(kBinThreads),
+                     (size_t)(2 << bg.shift) * sizeof(unsigned long long), (hipStream_t)stream, r);
+  return hip_status(hipGetLastError());
+}
+
 extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_args* a,
                                  void* workspace, size_t ws_bytes, void* stream) {
   int32_t st = check_cfg(cfg);
@@ -2759,6 +2977,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
       tv_atomic = true;
     }
   }
+  if (a->owner_defer && mode != kModeSplit) return HN_E_SHAPE;
   const WsLayout wl = ws_layout(cfg, a->n_rays, mode);
   BinGeom bg{};
   k.bins = nullptr;
@@ -2817,28 +3036,19 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.dc = a->d_coarse;
     sk.df = a->d_fine;
     sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
+    sk.merge_levels = merge_levels(cfg);
     hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), 0, s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
   if (mode != kModeAtomic) {
-    BinR r;
-    r.bins = k.bins;
-    r.n_rays = a->n_rays;
-    r.nbins = bg.nbins;
-    r.cap = bg.cap;
-    r.shift = bg.shift;
-    r.log2T = T;
-    r.d_table = a->d_table;
-    r.overwrite = (a->d_table_mode & 1) != 0;
-    r.fused = a->table_step != nullptr;
-    if (r.fused) r.step = *a->table_step;
-    r.live = r.fused ? a->table_live : nullptr;
-    r.live_levels = r.live ? a->table_live_levels : 0;
+    const BinR r = owner_args(cfg, a, k.bins, bg, 0);
     hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
     if ((st = hip_status(hipGetLastError()))) return st;
-    hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
-                       (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
-    if ((st = hip_status(hipGetLastError()))) return st;
+    if (!a->owner_defer) {
+      hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
+                         (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
+      if ((st = hip_status(hipGetLastError()))) return st;
+    }
   }
   if (mode != kModeSplit) {
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(kSlabVBlocks), dim3(64 * kSlabGroups), 0, s, slab, kBwdBlocks,

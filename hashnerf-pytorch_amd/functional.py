@@ -218,7 +218,7 @@ class RenderState:
     outputs, coarse origin of each fine sample, hash features, the workspace
     holding the packed weights)."""
     __slots__ = ("cfg", "rays", "noise_c", "noise_f", "table", "ws", "z_c", "z_f", "raw_c", "raw_f",
-                 "fine_src", "feat", "wsb", "nbytes")
+                 "fine_src", "feat", "wsb", "nbytes", "bwd_args")
 
 
 def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat):
@@ -263,11 +263,12 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
         st.cfg, st.rays, st.noise_c, st.noise_f, st.table, st.ws = cfg, rays, noise_c, noise_f, table, ws
         st.z_c, st.z_f, st.raw_c, st.raw_f = out["z_coarse"], out["z_fine"], out["raw_c"], out["raw_f"]
         st.fine_src, st.feat, st.wsb, st.nbytes = fine_src, feat, wsb, nbytes
+        st.bwd_args = None
     return out, st
 
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
-               overwrite_mlp: bool = False, tv=None, table_live=None):
+               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -282,7 +283,10 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     fused), or added to d_table -- instead of a separate tv_bwd.
     table_live = (n_levels, int32 bitmap) from train.live_pair_mask, with
     table_step: the fused step skips the row pairs no gradient can reach
-    (bitwise the same update, fewer optimizer-state bytes)."""
+    (bitwise the same update, fewer optimizer-state bytes).
+    owner_defer=True (binned scatter): the table gradient is not formed yet;
+    render_bwd_owner(st, lo, hi) then writes bins [lo, hi) (render_bins
+    gives their geometry), e.g. each range before its gradient exchange."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -335,9 +339,33 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
         g_tv = g_tv.contiguous()
         keep.append(g_tv)
         a.g_tv = g_tv.data_ptr()
+    a.owner_defer = 1 if owner_defer else 0
     t0 = TIMER.begin("render_bwd")
     L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
     TIMER.end("render_bwd", t0)
+    # the deferred owner pass reuses these arguments (and the buffers they point to)
+    st.bwd_args = (a, keep, step) if owner_defer else None
+    if CHECK_FAULTS and not owner_defer:
+        L.check_device_faults()
+
+
+def render_bins(cfg, n_rays: int):
+    """(number of bins, log2 table entries per bin) of the binned scatter
+    (hn_render_bins); (0, 0) for the float-atomic schedule."""
+    shift = C.c_int32(0)
+    n = L.lib().hn_render_bins(cfg, n_rays, C.byref(shift))
+    return int(n), int(shift.value)
+
+
+def render_bwd_owner(st: RenderState, bin_lo: int, bin_hi: int):
+    """hn_render_bwd_owner: the owner pass of a render_bwd(owner_defer=True)
+    over bins [bin_lo, bin_hi) -- their slices of d_table written (or
+    stepped, with table_step)."""
+    if getattr(st, "bwd_args", None) is None:
+        raise RuntimeError("hashnerf_amd.render_bwd_owner: needs a render_bwd(owner_defer=True) first")
+    a = st.bwd_args[0]
+    L.check(L.lib().hn_render_bwd_owner(st.cfg, a, L.ptr(st.wsb), st.nbytes, bin_lo, bin_hi,
+                                        L.stream(st.rays.device)), "render_bwd_owner")
     if CHECK_FAULTS:
         L.check_device_faults()
 

@@ -143,15 +143,17 @@ class Collectives:
         self.rank, self.world, self.group = rank, world, group
         self.emulate = dist.get_backend(group) == "gloo" if emulate is None else emulate
 
-    def reduce_scatter(self, out, inp):
+    def reduce_scatter(self, out, inp, async_op=False):
+        """Returns the RCCL work handle with async_op (None under gloo, whose
+        emulation completes in the call)."""
         n = out.numel()
         if inp.numel() != n * self.world:
             raise ValueError(f"reduce_scatter: input {inp.numel()} != {self.world} x output {n}")
         if self.emulate:
             dist.all_reduce(inp, group=self.group)
             out.copy_(inp[self.rank * n:(self.rank + 1) * n])
-        else:
-            dist.reduce_scatter_tensor(out, inp, group=self.group)
+            return None
+        return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
 
     def all_gather(self, out, inp):
         n = inp.numel()
@@ -178,8 +180,20 @@ class ShardedTableStep:
     packed coarse | pad]: the render backward writes the table gradient into
     its first part as usual, and the packed vector is the buffer from the
     tail on -- contiguous, no copy of the 60 MB tail.  The table parameter is
-    re-pointed into the parameter buffer, so the all-gather (in place) updates
-    the tail directly and the coarse live rows are scattered back (4 MB).
+    re-pointed into the parameter buffer, so the all-gather updates the tail
+    in place and the coarse live rows are scattered back (4 MB).
+
+    Segments (overlap with the backward).  With ``bins`` =
+    (nbins, shift) of the binned scatter, the vector is cut into up to
+    ``n_chunks`` segments at bin boundaries (each a multiple of world floats):
+    tail pieces, then [rest of the tail | packed coarse | pad].  Each segment
+    is reduce-scattered on its own, right after ``produce(k)`` has formed its
+    bins' gradient (the render backward's deferred owner pass over
+    ``seg_bins[k]``; segment 0's range also holds the coarse levels), so on
+    RCCL segment k's exchange runs while the owner pass reduces segment k+1.
+    A rank's shard is the concatenation of its slices of the segments (its
+    p / g / m / v shards all in that order); one segment is the plain
+    layout.
 
     The table's RAdam moments live for this rank's shard only.  They start
     from ``state`` (the optimizer's exp_avg / exp_avg_sq of the table, e.g.
@@ -189,7 +203,7 @@ class ShardedTableStep:
     gather_state(): RAdam.state_dict() refuses to write a checkpoint while the
     optimizer's full-size copy is stale (Trainer.sync_optimizer_state)."""
 
-    def __init__(self, table, live, rank, world, group=None, state=None, stepper=None):
+    def __init__(self, table, live, rank, world, group=None, state=None, stepper=None, bins=None, n_chunks=4):
         L_, R, F_ = table.shape
         self.table, self.rank, self.world, self.group = table, rank, world, group
         self.coll = Collectives(rank, world, group)
@@ -202,10 +216,16 @@ class ShardedTableStep:
         n = self.full - self.head + self.nc
         self.P = (n + world - 1) // world * world
         self.s = self.P // world
+        self.segs, self.seg_bins = self._segments(bins, n_chunks)
+        offs = [0]
+        for lo, hi in self.segs:
+            offs.append(offs[-1] + (hi - lo) // world)
+        self.shard_offs = offs
         dev = table.device
         self.gbuf = torch.zeros(self.head + self.P, dtype=torch.float32, device=dev)
         self.pbuf = torch.zeros(self.head + self.P, dtype=torch.float32, device=dev)
         self.g_shard = torch.empty(self.s, dtype=torch.float32, device=dev)
+        self.p_shard = torch.empty(self.s, dtype=torch.float32, device=dev)
         with torch.no_grad():
             self.pbuf[:self.full].copy_(table.data.reshape(-1))
         table.data = self.pbuf[:self.full].view(L_, R, F_)
@@ -217,17 +237,51 @@ class ShardedTableStep:
                 self.v.copy_(self._shard_of(state["exp_avg_sq"]))
         self.stale = False
 
-    def _shard_of(self, full):
-        """This rank's slice of a full-size table tensor packed like the
-        exchanged gradient ([dense tail | coarse live rows | zero pad])."""
+    def _segments(self, bins, n_chunks):
+        """[(lo, hi)] over the packed vector (offsets from ``head``) and each
+        segment's bins [(b_lo, b_hi)] (None without ``bins``)."""
+        if not bins or n_chunks <= 1:
+            return [(0, self.P)], None
+        nbins, shift = bins
+        bf = 2 << shift                              # floats per bin
+        tail = self.full - self.head
+        unit = self.world * bf
+        if self.head % bf or self.full % bf or tail < unit:
+            return [(0, self.P)], None
+        nu = tail // unit                            # whole units in the tail
+        k = min(n_chunks - 1, nu)
+        cuts = [0] + [unit * ((nu * (j + 1)) // k) for j in range(k)]
+        segs = [(cuts[j], cuts[j + 1]) for j in range(k)]
+        if cuts[-1] < self.P:
+            segs.append((cuts[-1], self.P))
+        b0 = self.head // bf
+        sb = [(0 if j == 0 else b0 + lo // bf, min(nbins, b0 + hi // bf) if hi <= tail else nbins)
+              for j, (lo, hi) in enumerate(segs)]
+        sb[-1] = (sb[-1][0], nbins)
+        return segs, sb
+
+    def _packed_vector(self, full):
+        """A full-size table tensor packed like the exchanged vector ([dense
+        tail | coarse live rows | zero pad], P floats)."""
         F_ = self.table.shape[2]
         flat = full.detach().reshape(-1).to(device=self.pbuf.device, dtype=torch.float32)
         parts = [flat[self.head:]]
         if self.nc:
             parts.append(flat[:self.head].view(-1, F_).index_select(0, self.rows).reshape(-1))
         packed = torch.cat(parts)
-        packed = torch.cat([packed, packed.new_zeros(self.P - packed.numel())])
-        return packed[self.rank * self.s:(self.rank + 1) * self.s]
+        return torch.cat([packed, packed.new_zeros(self.P - packed.numel())])
+
+    def _shard_slices(self, vec):
+        """This rank's slices of the segments of a packed vector (views)."""
+        out = []
+        for lo, hi in self.segs:
+            n = (hi - lo) // self.world
+            out.append(vec[lo + self.rank * n:lo + (self.rank + 1) * n])
+        return out
+
+    def _shard_of(self, full):
+        """This rank's shard of a full-size table tensor (segment order)."""
+        return torch.cat(self._shard_slices(self._packed_vector(full)))
 
     def grad_view(self):
         """Where the render backward writes the table gradient (overwrite)."""
@@ -238,18 +292,32 @@ class ShardedTableStep:
         return buf[self.full:self.full + self.nc].view(-1, F_)
 
     @torch.no_grad()
-    def step(self, coeffs):
+    def step(self, coeffs, produce=None):
         """After the backward: exchange the gradient, RAdam step on the shard
-        (hn_radam_step, the reference's per-element op forms), all-gather."""
+        (hn_radam_step, the reference's per-element op forms), all-gather.
+        ``produce(k)``: forms segment k's gradient first (the deferred owner
+        pass over seg_bins[k]); None = the gradient is complete."""
         F_ = self.table.shape[2]
+        vec_g, vec_p = self.gbuf[self.head:], self.pbuf[self.head:]
+        works = []
+        last = len(self.segs) - 1
+        for k, (lo, hi) in enumerate(self.segs):
+            if produce is not None:
+                produce(k)
+            if k == last and self.nc:   # the coarse levels' bins are in segment 0's range
+                torch.index_select(self.gbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.gbuf))
+            o0, o1 = self.shard_offs[k], self.shard_offs[k + 1]
+            works.append(self.coll.reduce_scatter(self.g_shard[o0:o1], vec_g[lo:hi], async_op=True))
+        # the shard's parameters (the table may have been loaded since the last step)
         if self.nc:
-            torch.index_select(self.gbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.gbuf))
             torch.index_select(self.pbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.pbuf))
-        lo = self.head + self.rank * self.s
-        self.coll.reduce_scatter(self.g_shard, self.gbuf[self.head:])
-        p_shard = self.pbuf[lo:lo + self.s]
-        self.stepper([(p_shard, self.g_shard, self.m, self.v, coeffs)])
-        self.coll.all_gather(self.pbuf[self.head:], p_shard)
+        torch.cat(self._shard_slices(vec_p), out=self.p_shard)
+        for w in works:
+            if w is not None:
+                w.wait()
+        self.stepper([(self.p_shard, self.g_shard, self.m, self.v, coeffs)])
+        for k, (lo, hi) in enumerate(self.segs):
+            self.coll.all_gather(vec_p[lo:hi], self.p_shard[self.shard_offs[k]:self.shard_offs[k + 1]])
         if self.nc:
             self.pbuf[:self.head].view(-1, F_).index_copy_(0, self.rows, self._packed_coarse(self.pbuf))
         self.stale = True
@@ -261,7 +329,8 @@ class ShardedTableStep:
         F_ = self.table.shape[2]
         for sh in (self.m, self.v):
             packed = torch.empty(self.P, dtype=torch.float32, device=sh.device)
-            self.coll.all_gather(packed, sh)
+            for k, (lo, hi) in enumerate(self.segs):
+                self.coll.all_gather(packed[lo:hi], sh[self.shard_offs[k]:self.shard_offs[k + 1]])
             full = torch.zeros(self.full, dtype=torch.float32, device=sh.device)
             full[self.head:] = packed[:self.full - self.head]
             if self.nc:
@@ -452,7 +521,12 @@ class Trainer:
         # explicit mode, world > 1: reduce-scatter / sharded RAdam / all-gather
         # of the table (ShardedTableStep) instead of all-reduce + full RAdam
         self.dp_sharded = True
+        # ... in this many bin-aligned segments, each exchanged as soon as the
+        # backward's owner pass has formed it (1: one exchange after the whole
+        # backward)
+        self.dp_chunks = 4
         self._xchg = None
+        self._owner_st = None
 
     def _train_image(self):
         """np.random.choice(i_train) (run_nerf.py:578) from the host generator."""
@@ -568,8 +642,10 @@ class Trainer:
         if self.world > 1 and self.dp_sharded:
             # the moments continue from the optimizer's (a resumed run's
             # checkpoint, or an earlier setup's gathered state)
+            nb, shift = HF.render_bins(self._cfg, a.N_rand)
             self._xchg = ShardedTableStep(table, self._live_rows(), self.rank, self.world,
-                                          state=self.optimizer.state.get(table))
+                                          state=self.optimizer.state.get(table),
+                                          bins=(nb, shift) if nb else None, n_chunks=self.dp_chunks)
             self.optimizer.sharded_state = self._xchg
             self._gtable = self._xchg.grad_view()
         else:
@@ -637,8 +713,12 @@ class Trainer:
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
-            # no zero fill of the 64 MiB buffer), TV included
-            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True, tv=tvb)
+            # no zero fill of the 64 MiB buffer), TV included; with a segmented
+            # DP exchange its owner pass runs per segment inside the exchange
+            defer = self._xchg is not None and self._xchg.seg_bins is not None
+            HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True, tv=tvb,
+                          owner_defer=defer)
+            self._owner_st = st if defer else None
             table.grad = self._gtable
         for p, g in zip(self._ws, self._gws):
             p.grad = g
@@ -688,7 +768,12 @@ class Trainer:
             mlp = [p for p in self.grad_vars if p.grad is not None]
             flat = torch.cat([p.grad.reshape(-1) for p in mlp])
             work = dist.all_reduce(flat, async_op=True)
-            self._xchg.step(coeffs)
+            st, self._owner_st = self._owner_st, None
+            produce = None
+            if st is not None:
+                sb = self._xchg.seg_bins
+                produce = lambda k: HF.render_bwd_owner(st, *sb[k])
+            self._xchg.step(coeffs, produce=produce)
             work.wait()
             off = 0
             for p in mlp:

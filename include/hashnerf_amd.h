@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 11
+#define HN_ABI_VERSION 12
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -147,7 +147,11 @@ typedef struct hn_render_cfg {
   int32_t bin_cap;        /* binned scatter: records per (producer block, bin) region, a
                              multiple of 64; 0 = sized from the batch.  Small values
                              exercise the shared overflow records (tests). */
-  int32_t reserved;
+  int32_t merge_levels;   /* binned scatter (ABI 12): levels 0..n-1 have their records merged
+                             per producer block before they are stored (one record per
+                             distinct entry word: the block's exact fixed-point sum, rounded
+                             once to fp32); 0 = automatic (the levels of at most 130 cells
+                             per axis), -1 = none, n > 0: levels 0..n-1 */
 } hn_render_cfg;
 
 #define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the
@@ -226,8 +230,22 @@ typedef struct hn_render_bwd_args {
    * NULL = every row stepped. */
   const uint32_t* table_live;
   int32_t table_live_levels;
-  int32_t reserved;
+  /* ABI 12, binned scatter only: nonzero = stop before the owner pass; the
+   * caller then runs it per range of bins with hn_render_bwd_owner (e.g. to
+   * start each range's gradient exchange while the next range is reduced).
+   * The workspace must not be touched in between. */
+  int32_t owner_defer;
 } hn_render_bwd_args;
+
+/* The binned scatter's bins for this cfg and batch: returns their number (0:
+ * the float-atomic schedule, no bins) and sets *shift: bin b holds the table
+ * entries (flat level-major rows) [b << shift, (b + 1) << shift). */
+int32_t hn_render_bins(const hn_render_cfg* cfg, int64_t n_rays, int32_t* shift);
+/* The owner pass of hn_render_bwd (owner_defer set) over bins [bin_lo,
+ * bin_hi): writes (or steps, with table_step) exactly those bins' slices of
+ * the table gradient.  Same cfg / args / workspace as the deferred call. */
+int32_t hn_render_bwd_owner(const hn_render_cfg* cfg, const hn_render_bwd_args* a, void* workspace,
+                            size_t ws_bytes, int32_t bin_lo, int32_t bin_hi, void* stream);
 
 /* ---- L4 hash-table total variation (loss.py:11-43), all levels at once ---
  * Level l samples the cube of (cube[l]+1)^3 grid vertices starting at

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(hn):
     for n in names:
         assert hasattr(lib, n), n
         assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
-    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 11
+    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 12
 
 
 def test_struct_sizes_match_header(hn):

@@ -197,7 +197,7 @@ def _toy_step(tensors):
         p.sub_(c["lr"] * m / (v.sqrt() + 1.0))
 
 
-def _sharded_worker(rank, world, port, out_path):
+def _sharded_worker(rank, world, port, out_path, n_chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import sys
@@ -228,12 +228,26 @@ def _sharded_worker(rank, world, port, out_path):
 
     # sharded: RCCL's call sequence, the collectives emulated on gloo
     table = torch.nn.Parameter(p0.clone())
+    # n_chunks > 1: bins of 16 rows (32 floats), the exchange in bin-aligned
+    # segments, each segment's gradient formed just before its exchange (the
+    # trainer's deferred owner pass) over a gradient buffer holding NaN
+    bins = (L_ * R // 16, 4) if n_chunks > 1 else None
     xs = ShardedTableStep(table, live, rank, world, state={"exp_avg": m0, "exp_avg_sq": v0},
-                          stepper=_toy_step)
+                          stepper=_toy_step, bins=bins, n_chunks=n_chunks)
     assert xs.coll.emulate
+    assert len(xs.segs) == (3 if n_chunks > 1 else 1)
     for step in range(3):
-        xs.grad_view().copy_(grads(step)[rank])
-        xs.step(c)
+        g = grads(step)[rank]
+        if n_chunks > 1:
+            xs.grad_view().fill_(float("nan"))
+
+            def produce(k, g=g):
+                lo, hi = xs.seg_bins[k]
+                xs.grad_view().view(-1)[lo * 32:hi * 32] = g.reshape(-1)[lo * 32:hi * 32]
+            xs.step(c, produce=produce)
+        else:
+            xs.grad_view().copy_(g)
+            xs.step(c)
     assert xs.stale
     m, v = xs.gather_state()
     assert not xs.stale
@@ -247,14 +261,16 @@ def _sharded_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_sharded_table_step_matches_dense(tmp_path):
+@pytest.mark.parametrize("n_chunks", [1, 3])
+def test_sharded_table_step_matches_dense(tmp_path, n_chunks):
     """train.ShardedTableStep through train.Collectives (gloo emulating
     reduce_scatter_tensor / all_gather_into_tensor into the RCCL call's own
     out-tensors and offsets): 3 steps from loaded moments (a resumed run) leave
     the table and the gathered moments equal to the summed-gradient dense
-    update; the dead coarse rows stay untouched."""
+    update; the dead coarse rows stay untouched.  n_chunks=3: the same in
+    bin-aligned segments, each formed (produce) right before its exchange."""
     port = _free_port()
-    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path / "sh.pt")), nprocs=2, join=True)
+    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path / "sh.pt"), n_chunks), nprocs=2, join=True)
     got = torch.load(tmp_path / "sh.pt", weights_only=True)
     torch.testing.assert_close(got["p"], got["pr"], rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(got["m"], got["mr"], rtol=1e-6, atol=1e-7)

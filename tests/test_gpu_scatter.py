@@ -122,6 +122,29 @@ def test_binned_overflow_records(hn):
     assert _rel(t_small, t_full) <= 1e-6, _rel(t_small, t_full)
 
 
+@pytest.mark.parametrize("box", ["chair", "clumped"])
+def test_merged_levels_match_unmerged(hn, box):
+    """hn_render_cfg.merge_levels: the coarse levels' records merged per
+    producer block (one record per distinct entry word, the block's exact
+    fixed-point sum rounded once) against every record stored: the same
+    gradient to fp32 rounding, each form bitwise reproducible.  16 merged
+    levels overflow the block's merge table on the fine levels (or exceed the
+    scale bound outside the clumped box), which then fall back to unmerged
+    records."""
+    bx = BOX if box == "chair" else (torch.tensor([-1.0, -1.0, -1.0]), torch.tensor([1.0, 1.0, 1.0]))
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 4096, 19, 11, "binned", box=bx)
+    out = {}
+    for n in (-1, 0, 4, 16):
+        st.cfg.merge_levels = n
+        t1, _ = _bwd(HF, emb, ws, st, grads)
+        t2, _ = _bwd(HF, emb, ws, st, grads)
+        assert torch.equal(t1, t2), f"merge_levels={n}: table gradient changed between identical launches"
+        out[n] = t1
+    assert torch.count_nonzero(out[-1]) > 0
+    for n in (0, 4, 16):
+        assert _rel(out[n], out[-1]) <= 1e-6, (n, _rel(out[n], out[-1]))
+
+
 def test_binned_clumped_box(hn):
     """scannet-style box (bench config 5): samples mostly outside the box,
     the regions of the surface voxels' bins spill; binned == atomic."""
@@ -208,6 +231,29 @@ def test_binned_vs_oracle_bench_shape(hn, oracle):
     for p, w_ref in ((dws[:5], wc), (dws[5:], wf)):
         for x, k in zip(p, O.MLP_KEYS):
             assert _rel(x, w_ref[k].grad) <= 5e-4, (k, _rel(x, w_ref[k].grad))
+
+
+def test_deferred_owner_ranges_bitwise(hn):
+    """render_bwd(owner_defer=True) + render_bwd_owner over bin ranges (the
+    data-parallel exchange's segments) writes exactly the table gradient of
+    the one-call backward, range by range: bins not yet run keep the buffer's
+    old contents."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 2048, 19, 9, "binned")
+    ref, _ = _bwd(HF, emb, ws, st, grads, overwrite=True)
+    nb, shift = HF.render_bins(st.cfg, 2048)
+    assert nb == 1024 and shift == 13
+    d = torch.full_like(emb.table, float("nan"))
+    HF.render_bwd(st, grads, d, HF.zeros_like_all(ws), overwrite=True, owner_defer=True)
+    flat, rflat, bf = d.view(-1), ref.view(-1), 2 << shift
+    cuts = [0, 300, 301, 777, nb]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        HF.render_bwd_owner(st, lo, hi)
+        torch.cuda.synchronize()
+        assert torch.equal(flat[:hi * bf], rflat[:hi * bf]), (lo, hi)
+        assert torch.isnan(flat[hi * bf:]).all()
+    HF.L.check_device_faults()
+    with pytest.raises(RuntimeError):
+        HF.render_bwd_owner(st, 0, nb + 1)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
