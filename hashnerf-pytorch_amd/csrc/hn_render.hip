@@ -1558,14 +1558,18 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     bool act;
     Ray r;
     float pt[3], xc[3];
-    float g0, g1;
+    const float* tb;   // the sample's fine grads (tile order)
+    const float* tw;   // its coarse twin's grads, or null
+    float g0, g1;      // the current level's two feature grads (fine + coarse twin)
   };
   bool bad = false;   // a non-finite grad or point seen by this lane
-  auto unit_at = [&](int64_t it, int l) {
+  // unit u0 + wave + it * kScWaves: its ray, the lane's sample point and grad rows
+  auto unit_base = [&](int64_t it) {
     Unit q;
     const int64_t u = u0 + wave + it * kScWaves;
     q.act = u < u1;
     q.g0 = q.g1 = 0.f;
+    q.tb = q.tw = nullptr;
     if (q.act) {
       const int64_t ray = u / 3;
       const int i = 64 * (int)(u % 3) + lane;       // fine sample
@@ -1573,24 +1577,30 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       ray_point(q.r, k.z_fine[ray * kSf + i], q.pt);
 #pragma unroll
       for (int a = 0; a < 3; ++a) q.xc[a] = clamp_t(q.pt[a], k.g.bmin[a], k.g.bmax[a]);
-      // level l = element 2 (l & 1) .. of level pair l / 2 (tile_level: chunk
-      // lp / 2 of lane half lp % 2)
-      const int lp = l >> 1, e = 2 * (l & 1);
-      const float* tb = k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024 +
-                        4 * (64 * (lp >> 1) + 32 * (lp & 1) + (i & 31)) + e;
-      float2 gq = *reinterpret_cast<const float2*>(tb);
+      q.tb = k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024 + 4 * (i & 31);
       const int src = k.fine_src[ray * kSf + i];
-      if (src < kSc) {                          // coarse twin: fine + coarse grads
-        const float2 t2 = *reinterpret_cast<const float2*>(
-            k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024 +
-            4 * (64 * (lp >> 1) + 32 * (lp & 1) + (src & 31)) + e);
-        gq = make_float2(gq.x + t2.x, gq.y + t2.y);
-      }
-      q.g0 = gq.x;
-      q.g1 = gq.y;
-      const float chk = (gq.x + gq.y) + (l == 0 ? (q.pt[0] + q.pt[1]) + q.pt[2] : 0.f);
-      bad |= !(fabsf(chk) <= 3.402823466e38f);
+      if (src < kSc) q.tw = k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024 + 4 * (src & 31);
+      bad |= !(fabsf((q.pt[0] + q.pt[1]) + q.pt[2]) <= 3.402823466e38f);
     }
+    return q;
+  };
+  // level l's grads = elements 2 (l & 1) .. of level pair l / 2 (tile_level:
+  // chunk lp / 2 of lane half lp % 2); a coarse twin adds its coarse grads
+  auto unit_grads = [&](Unit& q, int l) {
+    if (!q.act) return;
+    const int lp = l >> 1, o = 4 * (64 * (lp >> 1) + 32 * (lp & 1)) + 2 * (l & 1);
+    float2 gq = *reinterpret_cast<const float2*>(q.tb + o);
+    if (q.tw) {
+      const float2 t2 = *reinterpret_cast<const float2*>(q.tw + o);
+      gq = make_float2(gq.x + t2.x, gq.y + t2.y);
+    }
+    q.g0 = gq.x;
+    q.g1 = gq.y;
+    bad |= !(fabsf(gq.x + gq.y) <= 3.402823466e38f);
+  };
+  auto unit_at = [&](int64_t it, int l) {
+    Unit q = unit_base(it);
+    unit_grads(q, l);
     return q;
   };
   // The records of one level of a unit: voxel, run heads, per corner row the
@@ -1710,8 +1720,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
   if (n_merge < 16) st_init(n_merge, par);
   __syncthreads();
-  for (int l = 0; l < 16; ++l) {
-    if (l < n_merge) {
+  for (int l = 0; l < n_merge; ++l) {
+    {
       // scale 2^S: values < 2^(E_B) -> < 2^40 units, E_B the exponent of the bound
       const float bnd = 16.f * __uint_as_float(mh_bound[l]);
       const int eb = bnd > 0.f && bnd <= 3.0e38f ? ilogbf(bnd) + 1 : 0;
@@ -1752,19 +1762,23 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
         if (threadIdx.x == 0) mh_fail = 0u;
         for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kDirect, 1.f);
       }
-      if (l + 1 == n_merge && l + 1 < 16) st_init(l + 1, par);
       __syncthreads();   // the table is empty again
-    } else {
-      for (int64_t it = 0; it < n_it; ++it) {
-        level(unit_at(it, l), l, kStaged, 1.f);
-        __syncthreads();   // the phase's records are in the pool, its counts final
-        st_flush(l);
-        // the next phase's bins (other parity), counts unchanged by the flush
-        const int ln = it + 1 < n_it ? l : l + 1;
-        if (ln < 16) st_init(ln, par ^ 1);
-        __syncthreads();   // the pool is free again
-        par ^= 1;
-      }
+    }
+  }
+  // the other levels unit by unit (each unit's ray and rows loaded once),
+  // their records through the staging pool, one phase per (unit round, level)
+  for (int64_t it = 0; it < n_it && n_merge < 16; ++it) {
+    Unit q = unit_base(it);
+    for (int l = n_merge; l < 16; ++l) {
+      unit_grads(q, l);
+      level(q, l, kStaged, 1.f);
+      __syncthreads();   // the phase's records are in the pool, its counts final
+      st_flush(l);
+      // the next phase's bins (other parity), counts unchanged by the flush
+      const int ln = l + 1 < 16 ? l + 1 : (it + 1 < n_it ? n_merge : 16);
+      if (ln < 16) st_init(ln, par ^ 1);
+      __syncthreads();   // the pool is free again
+      par ^= 1;
     }
   }
   // non-finite inputs (NaN / Inf in a grad or the point): one test per lane
