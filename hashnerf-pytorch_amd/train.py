@@ -610,7 +610,16 @@ class Trainer:
             self._livem = None if lm is None else (lm[0], lm[1].to(self.device))
         return self._livem
 
+    def finish_table_grad(self):
+        """Run the backward's deferred owner pass over the bins it has not
+        reduced yet (the segmented DP exchange defers it; see step()), so
+        that table.grad holds the whole table gradient."""
+        st, self._owner_st = self._owner_st, None
+        if st is not None:
+            HF.render_bwd_owner(st, 0, HF.render_bins(self._cfg, st.rays.shape[0])[0])
+
     def allreduce_grads(self):
+        self.finish_table_grad()
         if self.world > 1:
             allreduce_grads(self.embed_fn.table, self.grad_vars, live=self._live_rows())
 
