@@ -212,38 +212,6 @@ HN_DEV void encode_level_off(const float* __restrict__ table, uint32_t lvl_row0,
   f0 = trilerp(e0, v.w);
   f1 = trilerp(e1, v.w);
 }
-// One level's gathers by x-pairs (the forward's encode): corners c and c + 4
-// (x0 and x0 + 1; the x prime is 1) hash to rows h and h ^ 1 when x0 is even
-// -- one aligned 16-byte pair.  So each x-pair is one 16-byte buffer load of
-// the pair holding h(x0), plus an 8-byte load of h(x0 + 1) that only the lanes
-// with an odd x0 make: the others get an out-of-range offset, which a buffer
-// load answers with zeros and no memory access.  A quarter fewer row accesses
-// in the vector L1 (whose one-line-per-cycle tag rate bounds the gathers)
-// for the same 8 load instructions; branch-free selects, the same values and
-// trilerp: bitwise encode_level_off.  (x0 is odd exactly when
-// h(x0 + 1) != h(x0) ^ 1: x0 + 1 then flips bit 1 too, which the mask keeps.)
-HN_DEV void encode_level_xpair(__amdgpu_buffer_rsrc_t rs, uint32_t lvl_row0, const Voxel& v, float& f0, float& f1) {
-  float e0[8], e1[8];
-  const bool odd = v.h[4] != (v.h[0] ^ 1u);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const uint32_t r = lvl_row0 + v.h[c];
-    const f32x4 q = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (r & ~1u) * 8u, 0, 0));
-    const uint32_t r4 = odd ? (lvl_row0 + v.h[c + 4]) * 8u : 0xfffffff0u;
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const f32x2 t = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, r4, 0, 0));
-    const bool hi = (r & 1u) != 0u;
-    e0[c] = hi ? q.z : q.x;
-    e1[c] = hi ? q.w : q.y;
-    e0[c + 4] = odd ? t.x : (hi ? q.x : q.z);   // even x0: h(x0 + 1) = h(x0) ^ 1
-    e1[c + 4] = odd ? t.y : (hi ? q.y : q.w);
-  }
-  f0 = trilerp(e0, v.w);
-  f1 = trilerp(e1, v.w);
-}
-HN_DEV __amdgpu_buffer_rsrc_t table_rsrc(const float* table, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(table), (short)0, (int)bytes, 0x00020000);
-}
 HN_DEV void atomic_add_row(float* table, uint32_t byte_off, float g0, float g1) {
   float* p = reinterpret_cast<float*>(reinterpret_cast<char*>(table) + byte_off);
   atomic_add_f32(p, g0);

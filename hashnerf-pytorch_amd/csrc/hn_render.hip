@@ -25,8 +25,8 @@
 
 #include <type_traits>
 
-#ifndef HN_XPAIR   // 1: the forward's gathers by x-pairs (encode_level_xpair), 0: 8 row loads per level
-#define HN_XPAIR 0
+#ifndef HN_SC_MERGE_DIAG   // diagnostic builds only: 1 = the merged levels' table inserts skipped (timing)
+#define HN_SC_MERGE_DIAG 0
 #endif
 
 namespace hn {
@@ -165,14 +165,14 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
   // (Software-pipelining the levels -- level m + 1 or m + 2's gathers issued
   // before level m's are consumed -- measured slower: render_fwd_kernel 0.310
   // -> 0.330 / 0.323 ms, r04b; the other three waves of the SIMD already hide
-  // the gathers' latency.)
+  // the gathers' latency.  Loading a level's x-pairs as 16-B buffer loads
+  // where both corners share an aligned pair of rows (4 + 4 loads instead
+  // of 8) measured 0.2777 vs 0.2823 ms before the coarse-twin reuse, and
+  // 0.2789 vs 0.2731 ms after it (r04h, r04l): not kept.)
   float xc[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) xc[a] = clamp_t(pt[a], g.bmin[a], g.bmax[a]);
   const uint32_t mask = (1u << g.log2T) - 1u;
-#if HN_XPAIR
-  const __amdgpu_buffer_rsrc_t rs = table_rsrc(table, (uint32_t)g.n_levels << (g.log2T + 3));
-#endif
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     const int l0 = tile_level(m, 0), l1 = tile_level(m, 1);
@@ -182,22 +182,10 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     Voxel v;
     voxel_level_rcp(pt, xc, gs, rg, g.bmin, mask, v);
     float f0, f1;
-#if HN_XPAIR
-    encode_level_xpair(rs, l << g.log2T, v, f0, f1);
-    asm volatile("" : "+v"(f0), "+v"(f1));   // the level's interpolation here: its 24 data registers die
-#else
     encode_level_off(table, l << g.log2T, v, f0, f1);
-#endif
     feat[2 * m] = f0;
     feat[2 * m + 1] = f1;
-#if HN_XPAIR
-    // one level's 4 + 4 loads in flight (24 data registers); the memory clobber
-    // keeps the next level's buffer loads below this level's use
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#else
     if (m & 1) __builtin_amdgcn_sched_barrier(0);   // <= 16 gathers in flight
-#endif
   }
 }
 
@@ -1433,6 +1421,7 @@ struct ScK {
   hn_mlp_grad dc, df;
   int32_t overwrite_mlp;
   int32_t merge_levels;    // levels 0 .. merge_levels-1: records merged per block (merge table)
+  int32_t mh_log2;         // log2 merge-table slots (sc_lds_bytes)
 };
 constexpr int kScWaves = 16;
 constexpr int kScMaxBinsLog2 = 13;
@@ -1458,11 +1447,23 @@ constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per 
 // wave cycles), not on the write traffic.
 constexpr int kStLog2 = 12, kStPool = 1 << kStLog2;   // 64 KiB of values + 16 KiB of words
 constexpr int kStMinLog2C = 3;                          // fewer than 8 records per bin: no staging
-// Merge table of the coarse levels (over the pool's LDS): entry words and
-// their 4 sums as 64-bit fixed point, 36 B per slot
-constexpr int kMhSlotsLog2 = 11, kMhSlots = 1 << kMhSlotsLog2;
+// Merge table of the coarse levels (over the pool's LDS, grown to 4,096
+// slots when the bins' counters leave room): entry words and their 4 sums as
+// 64-bit fixed point, 36 B per slot
 constexpr uint32_t kMhEmpty = 0xffffffffu;   // never an entry word (bits 26-27 are zero)
-static_assert(kMhSlots * 36 <= kStPool * 20, "the merge table fits the staging pool");
+static_assert((1 << 11) * 36 <= kStPool * 20, "a 2,048-slot merge table fits the staging pool");
+constexpr size_t kScStaticLds = 10 * 1024;   // the kernel's static LDS (checked at launch)
+constexpr size_t kLdsMax = 160 * 1024;
+// dynamic LDS of scatter_bins_kernel: the counters, then max(pool, table)
+static int sc_mh_log2(int nbins) {
+  const size_t cnt = (size_t)((nbins + 3) & ~3) * 4;
+  return kScStaticLds + cnt + ((size_t)36 << 12) <= kLdsMax ? 12 : 11;
+}
+static size_t sc_lds_bytes(int nbins) {
+  const size_t cnt = (size_t)((nbins + 3) & ~3) * 4, pool = (size_t)kStPool * 20;
+  const size_t tab = (size_t)36 << sc_mh_log2(nbins);
+  return cnt + (pool > tab ? pool : tab);
+}
 struct StPhase {
   int b0, log2c;   // first bin of the level, log2 pool records per bin (< kStMinLog2C: direct)
   int nbl;         // bins of the level
@@ -1477,7 +1478,10 @@ HN_DEV StPhase st_phase(int l, int log2T, int shift) {
 }
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
-  __shared__ uint32_t bcnt[kScMaxBins];
+  // dynamic LDS: the bins' record counters, then the staging pool / merge
+  // table (sc_lds_bytes)
+  extern __shared__ __attribute__((aligned(16))) uint32_t sc_dyn[];
+  uint32_t* const bcnt = sc_dyn;
   __shared__ float gsl[kGsLds], lvmx[16];
   __shared__ uint32_t lovf;
   __shared__ uint32_t lvmxl[16 * 64];
@@ -1511,11 +1515,12 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int pp = lane & 15;
   // the staging pool (fine levels) and, over the same LDS, the merge table
   // (merged levels): 80 KiB
-  __shared__ __attribute__((aligned(16))) uint32_t st_raw[kStPool * 5];
+  uint32_t* const st_raw = sc_dyn + ((k.nbins + 3) & ~3);   // 16-B aligned after the counters
   f32x4* const stv = reinterpret_cast<f32x4*>(st_raw);
   uint32_t* const stw = st_raw + 4 * kStPool;
-  uint32_t* const mh_w = st_raw;                                                      // [kMhSlots] words
-  unsigned long long* const mh_v = reinterpret_cast<unsigned long long*>(st_raw + kMhSlots);   // [4][kMhSlots]
+  const int mh_log2 = k.mh_log2, mh_n = 1 << mh_log2;     // merge table slots
+  uint32_t* const mh_w = st_raw;                                                   // [mh_n] words
+  unsigned long long* const mh_v = reinterpret_cast<unsigned long long*>(st_raw + mh_n);   // [4][mh_n]
   __shared__ uint32_t stfl[2][kStPool >> kStMinLog2C];   // per phase parity: first staged slot per bin
   __shared__ uint32_t mh_bound[16], mh_fail;
   const int log2T = (int)k.g.log2T, sh = k.bin_shift;
@@ -1546,10 +1551,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   };
   // the merge table empty (every merged level leaves it empty again)
   auto mh_clear = [&]() {
-    for (int s = threadIdx.x; s < kMhSlots; s += blockDim.x) {
+    for (int s = threadIdx.x; s < mh_n; s += blockDim.x) {
       mh_w[s] = kMhEmpty;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) mh_v[c * kMhSlots + s] = 0ull;
+      for (int c = 0; c < 4; ++c) mh_v[c * mh_n + s] = 0ull;
     }
   };
   const int64_t n_it = (u1 - u0 + kScWaves - 1) / kScWaves;   // the same for every wave of the block
@@ -1640,38 +1645,62 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
     }
     if (mode == kMerged) {
+#if HN_SC_MERGE_DIAG
+      if (head && __float_as_uint(v[0][0]) == 0x7fc00001u) mh_fail = 1u;   // (keeps v live)
+      return;
+#endif
       if (head) {
-        bool fail = false;
+        // the 4 corner rows' slots: their first probes in flight together (a
+        // plain read: most inserts find their word already there, and
+        // same-address reads broadcast where compare-and-swaps serialise),
+        // then a claim of the empty ones, then linear probing for the rest
+        uint32_t word[4], s[4], cur[4];
+        bool ok[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int j = c >> 1, kk = c & 1;
           const uint32_t yy = j ? y0 + kPrimeY : y0, zz = kk ? z0 + kPrimeZ : z0;
           const uint32_t flat = ((uint32_t)l << log2T) + ((cx ^ yy ^ zz) & ((1u << log2T) - 1u));
-          const uint32_t word = flat | (((uint32_t)__builtin_ctz(~cx) + 1u) << 28);
+          word[c] = flat | (((uint32_t)__builtin_ctz(~cx) + 1u) << 28);
           // every value must convert exactly (|v * scale| < 2^46): else the
           // level is redone unmerged
-          bool ok = true;
+          ok[c] = true;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) ok = ok && fabsf(v[c][e] * mscale) < 0x1p46f;
-          uint32_t s = (word * 0x9E3779B1u) >> (32 - kMhSlotsLog2);
-          int probes = 0;
-          while (ok) {   // linear probing over the whole table: fails only when it is full
-            uint32_t cur = kMhEmpty;
-            __hip_atomic_compare_exchange_strong(mh_w + s, &cur, word, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (cur == kMhEmpty || cur == word) break;
-            s = (s + 1u) & (kMhSlots - 1u);
-            ok = ++probes < kMhSlots;
-          }
-          if (!ok) {
-            fail = true;
-            continue;
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            __hip_atomic_fetch_add(mh_v + e * kMhSlots + s, (unsigned long long)fx_of(v[c][e], mscale),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          for (int e = 0; e < 4; ++e) ok[c] = ok[c] && fabsf(v[c][e] * mscale) < 0x1p46f;
+          s[c] = (word[c] * 0x9E3779B1u) >> (32 - mh_log2);
         }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cur[c] = __hip_atomic_load(mh_w + s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (cur[c] == kMhEmpty) {   // claim it (or find the same word another lane just claimed)
+            __hip_atomic_compare_exchange_strong(mh_w + s[c], &cur[c], word[c], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur[c] == kMhEmpty) cur[c] = word[c];
+          }
+        bool fail = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int probes = 1;
+          while (ok[c] && cur[c] != word[c]) {   // linear probing over the whole table: fails only when it is full
+            s[c] = (s[c] + 1u) & (uint32_t)(mh_n - 1);
+            ok[c] = probes++ < mh_n;
+            cur[c] = __hip_atomic_load(mh_w + s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur[c] == kMhEmpty) {
+              __hip_atomic_compare_exchange_strong(mh_w + s[c], &cur[c], word[c], __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (cur[c] == kMhEmpty) cur[c] = word[c];
+            }
+          }
+          fail = fail || !ok[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (ok[c])
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              __hip_atomic_fetch_add(mh_v + e * mh_n + s[c], (unsigned long long)fx_of(v[c][e], mscale),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (fail) mh_fail = 1u;
       }
       return;   // the flush reports the merged values' maximum
@@ -1734,14 +1763,14 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       if (!failed) {
         // one record per distinct entry word: the block's exact sum, rounded once to fp32
         float vmax = 0.f;
-        for (int s = threadIdx.x; s < kMhSlots; s += blockDim.x) {
+        for (int s = threadIdx.x; s < mh_n; s += blockDim.x) {
           const uint32_t word = mh_w[s];
           if (word == kMhEmpty) continue;
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[e] = ldexpf((float)(long long)mh_v[e * kMhSlots + s], -S);
-            mh_v[e * kMhSlots + s] = 0ull;
+            v[e] = ldexpf((float)(long long)mh_v[e * mh_n + s], -S);
+            mh_v[e * mh_n + s] = 0ull;
             vmax = fmaxf(vmax, fabsf(v[e]));
           }
           mh_w[s] = kMhEmpty;
@@ -1840,7 +1869,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   }
   if (k.slab) {   // the dW slabs are complete (the MLP-backward kernel ran before this one)
     float(*part)[64] = reinterpret_cast<float(*)[64]>(stv);   // the staging pool is free now
-    static_assert(sizeof(st_raw) >= sizeof(float) * kSlabGroups * 64 && 64 * kScWaves == 64 * kSlabGroups,
+    static_assert(kStPool * 20 >= sizeof(float) * kSlabGroups * 64 && 64 * kScWaves == 64 * kSlabGroups,
                   "slab-reduce blocks inside the scatter blocks");
     // the 292 slab blocks go to the scatter blocks as they finish (a counter
     // reset by render_comp_bwd_kernel): the sums do not depend on who runs them
@@ -3051,7 +3080,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.df = a->d_fine;
     sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
     sk.merge_levels = merge_levels(cfg);
-    hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), 0, s, sk);
+    sk.mh_log2 = sc_mh_log2(sk.nbins);
+    hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), sc_lds_bytes(sk.nbins), s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
   if (mode != kModeAtomic) {
