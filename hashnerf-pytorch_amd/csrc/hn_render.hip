@@ -2755,20 +2755,23 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
 // Backward schedule: cfg->scatter 1 = float atomics (fused), 2 = binned
 // (split), 0 = binned unless the environment sets HN_SCATTER=atomic.  The
 // binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 22).
-// Levels whose records the scatter merges per block (a prefix: the levels
-// of at most kMergeMaxCells cells per axis, where a block's 16 neighbouring
-// rays cross few distinct voxels; config 2: levels 0-9, 2.5-23x fewer records
-// per block, scripts/bin_stats.py --dups).  hn_render_cfg.merge_levels, or
-// HN_SC_MERGE_LEVELS=n when that is 0 (automatic), overrides.
+// Levels whose records the scatter merges per block (a prefix).  The
+// automatic choice (merge_levels = -1) takes the levels of at most
+// kMergeMaxCells cells per axis, where a block's 16 neighbouring rays cross
+// few distinct voxels (config 2: levels 0-9, 2.5-23x fewer records per
+// block, scripts/bin_stats.py --dups).  The default (0) merges none: merged,
+// the owner pass is faster but the table inserts cost more in the scatter
+// (config 2, r04n: scatter + owner 423 us unmerged, 429 / 440 / 442 us with
+// 4 / 7 / 10 levels merged).  HN_SC_MERGE_LEVELS=n sets the default.
 constexpr double kMergeMaxCells = 130.0;
 static int merge_levels(const hn_render_cfg* c) {
   static const int env = [] {
     const char* e = getenv("HN_SC_MERGE_LEVELS");
-    return e ? atoi(e) : -1;
+    return e ? atoi(e) : 0;
   }();
   const hn_grid& g = c->grid;
   const int want = c->merge_levels != 0 ? c->merge_levels : env;
-  if (want >= 0 || c->merge_levels < 0) return want < 0 ? 0 : (want < g.n_levels ? want : g.n_levels);
+  if (want >= 0) return want < g.n_levels ? want : g.n_levels;
   int n = 0;
   for (int l = 0; l < g.n_levels; ++l) {
     double cells = 0.0;

@@ -150,8 +150,9 @@ typedef struct hn_render_cfg {
   int32_t merge_levels;   /* binned scatter (ABI 12): levels 0..n-1 have their records merged
                              per producer block before they are stored (one record per
                              distinct entry word: the block's exact fixed-point sum, rounded
-                             once to fp32); 0 = automatic (the levels of at most 130 cells
-                             per axis), -1 = none, n > 0: levels 0..n-1 */
+                             once to fp32); n > 0: levels 0..n-1, -1 = the levels of at most
+                             130 cells per axis, 0 = the default: none (measured slower on
+                             MI355X), or HN_SC_MERGE_LEVELS from the environment */
 } hn_render_cfg;
 
 #define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the

@@ -124,7 +124,8 @@ def test_binned_overflow_records(hn):
 
 @pytest.mark.parametrize("box", ["chair", "clumped"])
 def test_merged_levels_match_unmerged(hn, box):
-    """hn_render_cfg.merge_levels: the coarse levels' records merged per
+    """hn_render_cfg.merge_levels (0 = none, the default; -1 = automatic;
+    n = levels 0..n-1): the coarse levels' records merged per
     producer block (one record per distinct entry word, the block's exact
     fixed-point sum rounded once) against every record stored: the same
     gradient to fp32 rounding, each form bitwise reproducible.  16 merged
@@ -134,15 +135,15 @@ def test_merged_levels_match_unmerged(hn, box):
     bx = BOX if box == "chair" else (torch.tensor([-1.0, -1.0, -1.0]), torch.tensor([1.0, 1.0, 1.0]))
     HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 4096, 19, 11, "binned", box=bx)
     out = {}
-    for n in (-1, 0, 4, 16):
+    for n in (0, -1, 4, 16):
         st.cfg.merge_levels = n
         t1, _ = _bwd(HF, emb, ws, st, grads)
         t2, _ = _bwd(HF, emb, ws, st, grads)
         assert torch.equal(t1, t2), f"merge_levels={n}: table gradient changed between identical launches"
         out[n] = t1
-    assert torch.count_nonzero(out[-1]) > 0
-    for n in (0, 4, 16):
-        assert _rel(out[n], out[-1]) <= 1e-6, (n, _rel(out[n], out[-1]))
+    assert torch.count_nonzero(out[0]) > 0
+    for n in (-1, 4, 16):
+        assert _rel(out[n], out[0]) <= 1e-6, (n, _rel(out[n], out[0]))
 
 
 def test_binned_clumped_box(hn):
