@@ -301,6 +301,8 @@ class ShardedTableStep:
         vec_g, vec_p = self.gbuf[self.head:], self.pbuf[self.head:]
         works = []
         last = len(self.segs) - 1
+        # (bench.py: the deferred owner pass's launches, bracketed on the compute stream)
+        t_own = HF.TIMER.begin("render_bwd_owner") if produce is not None else None
         for k, (lo, hi) in enumerate(self.segs):
             if produce is not None:
                 produce(k)
@@ -308,6 +310,7 @@ class ShardedTableStep:
                 torch.index_select(self.gbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.gbuf))
             o0, o1 = self.shard_offs[k], self.shard_offs[k + 1]
             works.append(self.coll.reduce_scatter(self.g_shard[o0:o1], vec_g[lo:hi], async_op=True))
+        HF.TIMER.end("render_bwd_owner", t_own)
         # the shard's parameters (the table may have been loaded since the last step)
         if self.nc:
             torch.index_select(self.pbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.pbuf))
