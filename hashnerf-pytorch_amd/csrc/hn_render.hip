@@ -25,6 +25,9 @@
 
 #include <type_traits>
 
+#ifndef HN_SC_XROW   // 1: the scatter folds runs that cross its 16-lane rows into one record
+#define HN_SC_XROW 0
+#endif
 #ifndef HN_SC_MERGE_DIAG   // diagnostic builds only: 1 = the merged levels' table inserts skipped (timing)
 #define HN_SC_MERGE_DIAG 0
 #endif
@@ -1624,7 +1627,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     voxel_cw_sc(k.g, gsl, q.pt, q.xc, l, cell, w);
     const uint32_t cx = (uint32_t)cell[0], y0 = (uint32_t)cell[1] * kPrimeY, z0 = (uint32_t)cell[2] * kPrimeZ;
     const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
-    const bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
+    bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
     const uint64_t hb = __ballot(head);
     const uint32_t pm = (uint32_t)(hb >> (lane & 48)) & 0xffffu;
     // lane 0 of every row is a head, so these never carry across rows
@@ -1642,8 +1645,43 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
       v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
       seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
+#if !HN_SC_XROW
       vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+#endif
     }
+#if HN_SC_XROW
+    // Runs that continue across the 16-lane rows: row r's first lane (a head
+    // only because rows are summed separately) is folded into the last run
+    // head of row r - 1, for r = 3, 2, 1 in that order (a run spanning several
+    // rows ends in its first row's head); a fixed order of fp32 adds, so the
+    // records stay a function of the unit's samples alone
+    {
+      uint64_t he = hb;
+#pragma unroll
+      for (int r = 3; r >= 1; --r) {
+        const int l0 = 16 * r;
+        const bool cont = __builtin_amdgcn_readlane((int)cx, l0) == __builtin_amdgcn_readlane((int)cx, l0 - 1) &&
+                          __builtin_amdgcn_readlane((int)y0, l0) == __builtin_amdgcn_readlane((int)y0, l0 - 1) &&
+                          __builtin_amdgcn_readlane((int)z0, l0) == __builtin_amdgcn_readlane((int)z0, l0 - 1);
+        if (cont) {   // wave-uniform
+          const uint32_t rm = (uint32_t)(he >> (l0 - 16)) & 0xffffu;   // row r - 1's heads (bit 0 always set)
+          const int t = l0 - 16 + 31 - __builtin_clz(rm);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[c][e]), l0));
+              v[c][e] = lane == t ? v[c][e] + s : v[c][e];
+            }
+          he &= ~(1ull << l0);
+        }
+      }
+      head = ((he >> lane) & 1ull) != 0ull;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+    }
+#endif
     if (mode == kMerged) {
 #if HN_SC_MERGE_DIAG
       if (head && __float_as_uint(v[0][0]) == 0x7fc00001u) mh_fail = 1u;   // (keeps v live)
