@@ -100,6 +100,41 @@ def test_argument_validation_without_gpu(hn):
     assert lib.hn_blender_images(None, 0, 4, 4, 1, 1, None, None) == 0
 
 
+def test_bins_and_deferred_owner_validation_without_gpu(hn):
+    """ABI 12: hn_render_bins reports the binned scatter's geometry (host
+    arithmetic only), and hn_render_bwd_owner rejects a call that did not
+    defer its owner pass, a bad bin range or missing buffers before any
+    launch."""
+    L = hn._lib
+    lib = L.lib()
+    HF = hn.functional
+    box = (torch.tensor([-1.5, -1.5, -1.5]), torch.tensor([1.5, 1.5, 1.5]))
+    for T, finest, want in ((19, 512, (1024, 13)), (22, 1024, (8192, 13)), (14, 512, (32, 13))):
+        emb = hn.HashEmbedder(box, log2_hashmap_size=T, finest_resolution=finest)
+        cfg = HF.make_render_cfg(emb.grid(), True, False, True, scatter="binned")
+        assert HF.render_bins(cfg, 4096) == want, (T, HF.render_bins(cfg, 4096))
+        cfg_a = HF.make_render_cfg(emb.grid(), True, False, True, scatter="atomic")
+        assert HF.render_bins(cfg_a, 4096) == (0, 0)
+    shift = C.c_int32(-1)
+    assert lib.hn_render_bins(None, 4096, C.byref(shift)) == 0
+    emb = hn.HashEmbedder(box, log2_hashmap_size=19, finest_resolution=512)
+    cfg = HF.make_render_cfg(emb.grid(), True, False, True, scatter="binned")
+    a = L.HnRenderBwdArgs()
+    a.n_rays = 4096
+    x = C.c_void_p(16)   # never dereferenced: validation happens before any launch
+    ws = lib.hn_render_workspace_bytes(cfg, 4096)
+    assert lib.hn_render_bwd_owner(cfg, None, x, ws, 0, 1, None) == 1          # no args
+    assert lib.hn_render_bwd_owner(cfg, a, None, ws, 0, 1, None) == 1          # no workspace
+    assert lib.hn_render_bwd_owner(cfg, a, x, ws, 0, 1, None) == 2             # owner_defer not set
+    a.owner_defer = 1
+    assert lib.hn_render_bwd_owner(cfg, a, x, ws, 0, 1, None) == 1             # neither d_table nor table_step
+    a.d_table = 16
+    assert lib.hn_render_bwd_owner(cfg, a, x, ws - 4, 0, 1, None) == 3         # workspace too small
+    assert lib.hn_render_bwd_owner(cfg, a, x, ws, 0, 1025, None) == 2          # past the last bin
+    assert lib.hn_render_bwd_owner(cfg, a, x, ws, 7, 3, None) == 2             # reversed range
+    assert lib.hn_render_bwd_owner(cfg, a, x, ws, 5, 5, None) == 0             # empty range: no-op
+
+
 def test_product_path_refuses_cpu_tensors(hn):
     emb = hn.HashEmbedder((torch.tensor([-1., -1, -1]), torch.tensor([1., 1, 1])), log2_hashmap_size=12)
     with pytest.raises(RuntimeError, match="ROCm"):
