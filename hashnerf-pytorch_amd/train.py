@@ -193,7 +193,9 @@ class ShardedTableStep:
     RCCL segment k's exchange runs while the owner pass reduces segment k+1.
     A rank's shard is the concatenation of its slices of the segments (its
     p / g / m / v shards all in that order); one segment is the plain
-    layout.
+    layout.  The stepped shards come back in ONE all-gather (rank-major, then
+    one strided copy per segment), so the segmentation adds reduce-scatter
+    calls only.
 
     The table's RAdam moments live for this rank's shard only.  They start
     from ``state`` (the optimizer's exp_avg / exp_avg_sq of the table, e.g.
@@ -231,6 +233,7 @@ class ShardedTableStep:
         table.data = self.pbuf[:self.full].view(L_, R, F_)
         self.m = torch.zeros(self.s, dtype=torch.float32, device=dev)
         self.v = torch.zeros(self.s, dtype=torch.float32, device=dev)
+        self._gath = None   # rank-major all-gather buffer (segmented exchange)
         if state is not None and "exp_avg" in state:
             with torch.no_grad():
                 self.m.copy_(self._shard_of(state["exp_avg"]))
@@ -319,8 +322,19 @@ class ShardedTableStep:
             if w is not None:
                 w.wait()
         self.stepper([(self.p_shard, self.g_shard, self.m, self.v, coeffs)])
-        for k, (lo, hi) in enumerate(self.segs):
-            self.coll.all_gather(vec_p[lo:hi], self.p_shard[self.shard_offs[k]:self.shard_offs[k + 1]])
+        if len(self.segs) == 1:   # the shard is one slice of the vector: gathered in place
+            self.coll.all_gather(vec_p, self.p_shard)
+        else:
+            # one all-gather (one collective call, not one per segment) into a
+            # rank-major buffer, then each segment's [world, n_k] block copied
+            # into place
+            if self._gath is None:
+                self._gath = torch.empty(self.P, dtype=torch.float32, device=self.pbuf.device)
+            self.coll.all_gather(self._gath, self.p_shard)
+            g2 = self._gath.view(self.world, self.s)
+            for k, (lo, hi) in enumerate(self.segs):
+                o0, o1 = self.shard_offs[k], self.shard_offs[k + 1]
+                vec_p[lo:hi].view(self.world, o1 - o0).copy_(g2[:, o0:o1])
         if self.nc:
             self.pbuf[:self.head].view(-1, F_).index_copy_(0, self.rows, self._packed_coarse(self.pbuf))
         self.stale = True
