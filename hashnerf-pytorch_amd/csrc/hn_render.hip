@@ -25,6 +25,16 @@
 
 #include <type_traits>
 
+#ifndef HN_FWD_PRIO   // > 0: the forward's waves raise their issue priority (s_setprio) while they encode
+#define HN_FWD_PRIO 0
+#endif
+#if HN_FWD_PRIO
+#define HN_FWD_PRIO_HI() __builtin_amdgcn_s_setprio(HN_FWD_PRIO)
+#define HN_FWD_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define HN_FWD_PRIO_HI() ((void)0)
+#define HN_FWD_PRIO_LO() ((void)0)
+#endif
 #ifndef HN_SC_XROW   // 1: the scatter folds runs that cross its 16-lane rows into one record
 #define HN_SC_XROW 0
 #endif
@@ -313,7 +323,9 @@ void render_fwd_kernel(RenderK k) {
     float pt[3];
     ray_point(r, zc[q], pt);
     f32x16 feat;
+    HN_FWD_PRIO_HI();
     encode_tile(k.g, gsl, k.table, pt, h, feat);
+    HN_FWD_PRIO_LO();
     HN_FT_FEAT(0, feat);
     if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
     MlpAct a;
@@ -379,7 +391,9 @@ void render_fwd_kernel(RenderK k) {
     // slower: 0.301 ms, the waves then run their MLP tiles in step (r04j).
     const int src = k.feat ? (int)k.fine_src[ray * kSf + q] : 255;
     if (src >= kSc) {
+      HN_FWD_PRIO_HI();
       encode_tile(k.g, gsl, k.table, pt, h, feat);
+      HN_FWD_PRIO_LO();
     } else {
       const f32x4* t = reinterpret_cast<const f32x4*>(k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY +
                                                       (size_t)(src >> 5) * 1024) + (src & 31) + 32 * h;
