@@ -41,6 +41,9 @@
 #define HN_FWD_PRIO_HI() ((void)0)
 #define HN_FWD_PRIO_LO() ((void)0)
 #endif
+#ifndef HN_ENC_GROUP   // levels per scheduling group of the forward's encode (8 gathers each)
+#define HN_ENC_GROUP 2
+#endif
 #ifndef HN_OWN_PRIO   // diagnostic A/B: > 0 = the owner pass's waves raise their priority while they issue record loads
 #define HN_OWN_PRIO 0
 #endif
@@ -214,7 +217,7 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     encode_level_off(table, l << g.log2T, v, f0, f1);
     feat[2 * m] = f0;
     feat[2 * m + 1] = f1;
-    if (m & 1) __builtin_amdgcn_sched_barrier(0);   // <= 16 gathers in flight
+    if ((m & (HN_ENC_GROUP - 1)) == HN_ENC_GROUP - 1) __builtin_amdgcn_sched_barrier(0);   // <= 8 x HN_ENC_GROUP gathers in flight
   }
 }
 
