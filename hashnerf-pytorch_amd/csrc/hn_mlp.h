@@ -36,9 +36,6 @@ namespace hn {
 // weight-gradient GEMMs.  0 = f32 MFMA (an exact FMA chain).  color_net.2^T
 // (4 k-steps, 2 used) is always f32 (a 2-part split of its 3 rgb grads as one
 // K = 16 chunk measured no faster: 1.154-1.155 ms vs 1.159 ms per step, r03g).
-#ifndef HN_FRAG_PRIO   // diagnostic A/B: > 0 = raise the wave's priority while it issues a chunk's weight-fragment loads
-#define HN_FRAG_PRIO 0
-#endif
 #ifndef HN_SPLIT_F
 #define HN_SPLIT_F 3
 #endif
@@ -103,14 +100,8 @@ HN_DEV f32x16 gemm_src(const Src& src, int ob, f32x16 acc, int lane, BF bval) {
 #pragma unroll
     for (int c = 0; c < KS / 8; ++c) {
       SP<NS> a;
-#if HN_FRAG_PRIO
-      __builtin_amdgcn_s_setprio(HN_FRAG_PRIO);
-#endif
 #pragma unroll
       for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(ld(NS * c + q));
-#if HN_FRAG_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
       acc = mfma_split<NS>(a, b, acc);
       __builtin_amdgcn_sched_barrier(0);

@@ -44,16 +44,6 @@
 #ifndef HN_ENC_GROUP   // levels per scheduling group of the forward's encode (8 gathers each)
 #define HN_ENC_GROUP 2
 #endif
-#ifndef HN_OWN_PRIO   // diagnostic A/B: > 0 = the owner pass's waves raise their priority while they issue record loads
-#define HN_OWN_PRIO 0
-#endif
-#if HN_OWN_PRIO
-#define HN_OWN_PRIO_HI() __builtin_amdgcn_s_setprio(HN_OWN_PRIO)
-#define HN_OWN_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#else
-#define HN_OWN_PRIO_HI() ((void)0)
-#define HN_OWN_PRIO_LO() ((void)0)
-#endif
 #ifndef HN_SC_XROW   // 1: the scatter folds runs that cross its 16-lane rows into one record
 #define HN_SC_XROW 0
 #endif
@@ -1868,9 +1858,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // the other levels unit by unit (each unit's ray and rows loaded once),
   // their records through the staging pool, one phase per (unit round, level)
   for (int64_t it = 0; it < n_it && n_merge < 16; ++it) {
-    HN_OWN_PRIO_HI();
     Unit q = unit_base(it);
-    HN_OWN_PRIO_LO();
     for (int l = n_merge; l < 16; ++l) {
       unit_grads(q, l);
       level(q, l, kStaged, 1.f);
@@ -2715,14 +2703,10 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   if (r0 < total) fetch(r0, va, wa);
   for (; r0 < total; r0 += 2 * kBrDepth * kBinThreads) {
     const uint32_t r1 = r0 + kBrDepth * kBinThreads;
-    HN_OWN_PRIO_HI();
     if (r1 < total) fetch(r1, vb, wb);
-    HN_OWN_PRIO_LO();
     add(r0, va, wa);
     if (r1 >= total) break;
-    HN_OWN_PRIO_HI();
     if (r1 + kBrDepth * kBinThreads < total) fetch(r1 + kBrDepth * kBinThreads, va, wa);
-    HN_OWN_PRIO_LO();
     add(r1, vb, wb);
   }
   if (n_ovf) {   // this bin's spilled records (bucketed by ovf_place_kernel)
