@@ -34,9 +34,6 @@
 #ifndef HN_FWD_PRIO
 #define HN_FWD_PRIO 1
 #endif
-#ifndef HN_FWD_PRIO_WIDE   // A/B: 1 = the fine tiles' priority also covers the coarse-twin feature loads
-#define HN_FWD_PRIO_WIDE 0
-#endif
 #if HN_FWD_PRIO
 #define HN_FWD_PRIO_HI() __builtin_amdgcn_s_setprio(HN_FWD_PRIO)
 #define HN_FWD_PRIO_LO() __builtin_amdgcn_s_setprio(0)
@@ -401,18 +398,11 @@ void render_fwd_kernel(RenderK k) {
     // importance samples as 4 full tiles first and loading every fine tile's
     // features back from the cache (a third fewer encode instructions) measured
     // slower: 0.301 ms, the waves then run their MLP tiles in step (r04j).
-#if HN_FWD_PRIO_WIDE
-    HN_FWD_PRIO_HI();
-#endif
     const int src = k.feat ? (int)k.fine_src[ray * kSf + q] : 255;
     if (src >= kSc) {
-#if !HN_FWD_PRIO_WIDE
       HN_FWD_PRIO_HI();
-#endif
       encode_tile(k.g, gsl, k.table, pt, h, feat);
-#if !HN_FWD_PRIO_WIDE
       HN_FWD_PRIO_LO();
-#endif
     } else {
       const f32x4* t = reinterpret_cast<const f32x4*>(k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY +
                                                       (size_t)(src >> 5) * 1024) + (src & 31) + 32 * h;
@@ -422,9 +412,6 @@ void render_fwd_kernel(RenderK k) {
         feat[4 * c] = v.x; feat[4 * c + 1] = v.y; feat[4 * c + 2] = v.z; feat[4 * c + 3] = v.w;
       }
     }
-#if HN_FWD_PRIO_WIDE
-    HN_FWD_PRIO_LO();
-#endif
     HN_FT_FEAT(3, feat);
     if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
     MlpAct a;
