@@ -673,6 +673,12 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
 // 0.812 -> 0.789 ms, step 1.159 -> 1.134 ms; the kernel's 24 VGPR spills go to 0.
 // The same pipelining in the forward's gemm (round 3, removed) changed
 // nothing there (render_fwd 0.304 ms either way).
+#ifndef HN_SWP_V1   // VALU per MFMA slot of the 2-part split pipelining (gemm_w / gemm_w2)
+#define HN_SWP_V1 7
+#endif
+#ifndef HN_SWP_V2
+#define HN_SWP_V2 4
+#endif
 template <int NMFMA, int NVALU>
 HN_DEV void swp_pattern() {
   static_for<0, NMFMA>([&](auto) {
@@ -703,7 +709,7 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
       acc = mfma_split<NS>(a, b, acc);
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 6 : 3, NS == 3 ? 6 : 7>();
+        swp_pattern<NS == 3 ? 6 : 3, NS == 3 ? 6 : HN_SWP_V1>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -758,7 +764,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : 4>();
+        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : HN_SWP_V2>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
