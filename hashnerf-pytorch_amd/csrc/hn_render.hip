@@ -673,12 +673,9 @@ HN_DEV f32x4 wring_take(WRing& w, const float* P, int lane) {
 // 0.812 -> 0.789 ms, step 1.159 -> 1.134 ms; the kernel's 24 VGPR spills go to 0.
 // The same pipelining in the forward's gemm (round 3, removed) changed
 // nothing there (render_fwd 0.304 ms either way).
-#ifndef HN_SWP_V1   // VALU per MFMA slot of the 2-part split pipelining (gemm_w / gemm_w2)
-#define HN_SWP_V1 7
-#endif
-#ifndef HN_SWP_V2
-#define HN_SWP_V2 4
-#endif
+// (VALU per MFMA slot, 2-part splits: 7 in gemm_w, 4 in gemm_w2.  Measured
+// round 4, r04sw: 5 / 3 took render_bwd_kernel from 0.2343 to 0.2426 ms,
+// 10 / 6 to 0.2364 ms.)
 template <int NMFMA, int NVALU>
 HN_DEV void swp_pattern() {
   static_for<0, NMFMA>([&](auto) {
@@ -709,7 +706,7 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
       acc = mfma_split<NS>(a, b, acc);
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 6 : 3, NS == 3 ? 6 : HN_SWP_V1>();
+        swp_pattern<NS == 3 ? 6 : 3, NS == 3 ? 6 : 7>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -764,7 +761,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : HN_SWP_V2>();
+        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : 4>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
