@@ -1,6 +1,6 @@
 """Headline benchmark: training rays/s (fwd+bwd) of the HashNeRF step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5]
 
 N = 1 runs BASELINE.json configs[1] (chair, N_rand 4096, 64+128 samples,
 L=16 F=2 T=2^19 finest 512) on one MI355X.  N > 1 is launched by torchrun
@@ -11,6 +11,10 @@ A step is one full training iteration: on-device ray sampling from a
 synthetic 400x400 image set resident in HBM, fused render forward, loss
 (MSE fine+coarse, entropy sparsity, TV), fused backward, gradient
 all-reduce (N > 1), RAdam step, lr decay.  Rank 0 prints one JSON line.
+--config 1 is BASELINE configs[0] (configs/chair.txt verbatim on the CPU
+PyTorch path): the oracle's training step (the CPU restatement of the
+reference, oracle/) at N_rand 1024, T=2^19, finest 512, precrop window, on
+the host cores; it touches no GPU.
 TV follows the reference's schedule (run_nerf.py:636-638: through i = 1001),
 so the timed steps after the 1000 untimed ones have none -- except config 3,
 whose BASELINE entry asks for the TV term on every step.  With one GPU and no
@@ -31,6 +35,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
+    # configs/chair.txt:1-19 verbatim: N_rand 1024, 64+128, precrop 500 @ 0.5,
+    # lrate 0.01 (README.md:20), T=19, finest 512; the reference's pure-PyTorch
+    # CPU path (BASELINE configs[0]: "plumbing, no GPU")
+    1: dict(workload="configs/chair.txt on the CPU PyTorch path: N_rand=1024, 64+128, T19 finest512, "
+                     "precrop 0.5 (BASELINE configs[0])",
+            N_rand=1024, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6),
     2: dict(workload="chair 1xMI355X N_rand=4096 64+128 L16 F2 T19 finest512 (BASELINE configs[1])",
             N_rand=4096, log2_hashmap_size=19, finest_res=512, tv_loss_weight=1e-6),
     3: dict(workload="lego T22 finest1024 N_rand=8192 TV on (BASELINE configs[2])",
@@ -104,24 +114,22 @@ def mfma_busy(ks, kernel, source):
             "grbm_gui_active": grbm, "source": source}
 
 
-def cpu_baseline(cfg, steps=3, n_rays=None, warm_rays=256):
-    """Oracle (torch-CPU restatement of the reference) training step on the
-    config's own shape: n_rays = the config's N_rand rays per step (SURVEY
-    8(d): >= 3 timed steps at each config's B, after one warm-up step), same
-    table size, the config's loss terms (sparsity weight, TV on every step for
-    config 3, the bbox and background), fwd + bwd + RAdam.  The warm-up step
-    runs warm_rays rays (the same code path; it only pays first-call costs)."""
+def _oracle_trainer(cfg, seed=0):
+    """The oracle's training state and one training step on the host
+    (test infrastructure: the CPU restatement of the reference path, oracle/):
+    returns step(i, n_rays, precrop) -> None.  Synthetic blender-style
+    cameras at 400 x 400, uniform targets, the config's table size, loss terms
+    (sparsity weight, TV while i <= tv_until, bbox and background), fwd + bwd
+    + RAdam with the reference's lr decay (run_nerf.py:647-651)."""
     import numpy as np
 
     from oracle import hashnerf_oracle as O
 
-    threads = torch.get_num_threads()
-    n_rays = n_rays or cfg["N_rand"]
     T, finest = cfg["log2_hashmap_size"], cfg["finest_res"]
     white = cfg.get("white_bkgd", True)
     sparse_w = cfg.get("sparse_loss_weight", 1e-10)
-    tv_w = cfg["tv_loss_weight"] if cfg.get("tv_until", 1001) > 1001 else 0.0   # timed steps follow pretraining
-    g = torch.Generator().manual_seed(0)
+    tv_w, tv_until = cfg["tv_loss_weight"], cfg.get("tv_until", 1001)
+    g = torch.Generator().manual_seed(seed)
     box = tuple(torch.tensor(v) for v in cfg["bbox"]) if "bbox" in cfg else \
         (torch.tensor([-4.02, -4.02, -3.34]), torch.tensor([4.02, 4.02, 3.24]))
     tab = ((torch.rand(16, 2 ** T, 2, generator=g) * 2 - 1) * 1e-4).requires_grad_(True)
@@ -133,19 +141,24 @@ def cpu_baseline(cfg, steps=3, n_rays=None, warm_rays=256):
     H = W = 400
     focal = .5 * W / np.tan(.5 * 0.6911112070083618)
     K = np.array([[focal, 0, 0.5 * W], [0, focal, 0.5 * H], [0, 0, 1]])
+    lrate, decay = 0.01, cfg.get("lrate_decay", 10)
 
-    def step(i, n):
+    def step(i, n, precrop=False):
         c2w = O.pose_spherical(float(i * 37 % 360 - 180), -30.0, 4.0)
         ro, rd = O.get_rays(H, W, K, c2w[:3, :4])
-        sel = torch.randperm(H * W, generator=g)[:n]
-        ro, rd = ro.reshape(-1, 3)[sel], rd.reshape(-1, 3)[sel]
+        if precrop:   # run_nerf.py:586-595: the centre 2dH x 2dW window, precrop_frac 0.5
+            dH = dW = int(H // 2 * 0.5)
+            ro, rd = ro[H // 2 - dH:H // 2 + dH, W // 2 - dW:W // 2 + dW], rd[H // 2 - dH:H // 2 + dH, W // 2 - dW:W // 2 + dW]
+        ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+        sel = torch.randperm(ro.shape[0], generator=g)[:n]   # without replacement (:600)
+        ro, rd = ro[sel], rd[sel]
         vd = rd / torch.norm(rd, dim=-1, keepdim=True)
         rb = torch.cat([ro, rd, 2 * torch.ones(n, 1), 6 * torch.ones(n, 1), vd], -1)
         ret = O.render_rays(rb, wc, wf, tab, box[0], box[1], res, T,
                             t_rand=torch.rand(n, 64, generator=g),
                             u=torch.rand(n, 128, generator=g), white_bkgd=white)
         loss = O.training_loss(ret, torch.rand(n, 3, generator=g), sparse_w)
-        if tv_w:
+        if tv_w and i <= tv_until:
             for l in range(16):                        # run_nerf.py:628-635, loss.py:22-25
                 r, cube = O.tv_cube(l, 16, 16, finest)
                 mv = torch.randint(0, int(r - cube), (3,), generator=g)
@@ -153,20 +166,92 @@ def cpu_baseline(cfg, steps=3, n_rays=None, warm_rays=256):
         for p in params:
             p.grad = None
         loss.backward()
+        lr = lrate * (0.1 ** ((i - 1) / (decay * 1000)))   # set after the previous step (:647-651)
         with torch.no_grad():
             for p, (m, v) in zip(params, state):
-                O.radam_step(p, p.grad, m, v, i + 1, 0.01, weight_decay=1e-6 if p is not tab else 0.0,
+                O.radam_step(p, p.grad, m, v, i, lr, weight_decay=1e-6 if p is not tab else 0.0,
                              eps=1e-15 if p is tab else 1e-8)
 
-    step(0, warm_rays)                        # warm-up (first-call costs)
+    return step
+
+
+def cpu_baseline(cfg, steps=3, n_rays=None, warm_rays=256):
+    """Oracle (torch-CPU restatement of the reference) training step on the
+    config's own shape: n_rays = the config's N_rand rays per step (SURVEY
+    8(d): >= 3 timed steps at each config's B, after one warm-up step), same
+    table size, the config's loss terms (sparsity weight, TV on every step for
+    config 3, the bbox and background), fwd + bwd + RAdam.  The warm-up step
+    runs warm_rays rays (the same code path; it only pays first-call costs).
+    The timed steps are numbered past the TV window, as the GPU's timed steps
+    follow 1000 pretraining steps."""
+    threads = torch.get_num_threads()
+    n_rays = n_rays or cfg["N_rand"]
+    T, finest = cfg["log2_hashmap_size"], cfg["finest_res"]
+    tv = cfg.get("tv_until", 1001) > 1001
+    step = _oracle_trainer(cfg)
+    step(1001, warm_rays)                     # warm-up (first-call costs)
     t0 = time.perf_counter()
     for i in range(steps):
-        step(i + 1, n_rays)
+        step(1002 + i, n_rays)
     dt = time.perf_counter() - t0
     return {"value": round(steps * n_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
             "sample": f"{steps} oracle training steps x {n_rays} rays (the config's B; T=2^{T}, finest {finest}, "
-                      f"64+128, fwd+bwd+RAdam{', TV' if tv_w else ''}) on {threads} host threads after a "
+                      f"64+128, fwd+bwd+RAdam{', TV' if tv else ''}) on {threads} host threads after a "
                       f"{warm_rays}-ray warm-up step, {dt:.1f} s"}
+
+
+def bench_config1(args):
+    """BASELINE configs[0]: configs/chair.txt verbatim on the CPU PyTorch path
+    (the oracle: the reference's algorithm restated in torch-CPU eager ops, as
+    the reference runs it on a CPU).  Steps 1..K of a fresh run: N_rand 1024
+    from the 200 x 200 precrop window (i < precrop_iters = 500), TV on
+    (i <= 1001), RAdam (no update before step 6), lr decay; one warm-up step
+    first.  Prints one JSON line; no GPU is touched."""
+    cfg = dict(CONFIGS[1], lrate_decay=500)          # configs/chair.txt:10
+    threads = torch.get_num_threads()
+    B = args.n_rand or cfg["N_rand"]
+    step = _oracle_trainer(cfg)
+    t0 = time.perf_counter()
+    step(1, B, precrop=True)                         # warm-up: the run's first step
+    warm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(2 + i, B, precrop=True)
+    dt = time.perf_counter() - t0
+    value = args.steps * B / dt
+    line = {
+        "metric": "training rays/sec (fwd+bwd) on chair; PSNR@5k iters",
+        "value": round(value, 2), "unit": "rays/s", "n_gpus": 0, "steps": args.steps, "warmup": 1,
+        "ms_per_step": round(dt * 1e3 / args.steps, 1), "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "fp32", "device": f"cpu ({threads} threads)",
+        "data": "synthetic: blender-style 400x400 cameras, uniform targets (no dataset in the image)",
+        "config": {"workload": cfg["workload"], "rays_per_step": B, "samples_per_ray": "64+128",
+                   "log2_hashmap_size": 19, "finest_res": 512, "precrop": "steps 1..499, frac 0.5",
+                   "lrate_decay": 500, "parallelism": "none"},
+        "path": "oracle/hashnerf_oracle.py: the reference's hot path restated op for op in torch-CPU "
+                "(pinned by reference-made golden fixtures, tests/test_oracle_golden.py)",
+        "roofline": None,
+        "cpu_baseline": {"value": round(value, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+                         "sample": f"{args.steps} training steps x {B} rays after a {warm:.1f} s warm-up step"},
+    }
+    print(json.dumps(line), flush=True)
+
+
+def optimizer_bytes(tr):
+    """HBM bytes the fused table RAdam step must move per launch: p, m and v
+    (fp32) read and written for every table parameter it steps -- the dense
+    levels whole, the coarse levels' live row pairs only (train.live_pair_mask,
+    Trainer.skip_dead_rows)."""
+    e = tr.embed_fn
+    T, L_, F_ = e.log2_hashmap_size, e.n_levels, 2
+    total = L_ * (1 << T) * F_
+    lm = tr._live_mask()
+    if lm is not None:
+        n_lv, words = lm
+        import numpy as np
+        live_pairs = int(np.unpackbits(words.cpu().numpy().view(np.uint8)).sum())
+        total = (L_ - n_lv) * (1 << T) * F_ + live_pairs * 2 * F_
+    return total * 4 * 3 * 2
 
 
 def _free_port():
@@ -206,16 +291,25 @@ def main():
                     help="uniform: random targets; procedural: train.procedural_field chair images")
     ap.add_argument("--pretrain", type=int, default=1000,
                     help="untimed training steps before warmup")
+    ap.add_argument("--kernel-steps", type=int, default=5,
+                    help="steps after the timed region whose launches are timed with HIP events (roofline)")
     ap.add_argument("--cpu-steps", type=int, default=3,
                     help="timed oracle steps of the CPU baseline, each at the config's N_rand")
     ap.add_argument("--ray-order", type=int, default=1, choices=(0, 1),
                     help="batch order from the sampler: 1 Morton order of the pixels, 0 draw order")
     ap.add_argument("--dense-table-step", action="store_true",
                     help="A/B: the fused table step over every row (no live-pair mask)")
+    ap.add_argument("--dp-chunks", type=int, default=1,
+                    help="N > 1: segments of the sharded table exchange, each reduce-scattered as soon as "
+                         "the owner pass has formed it (1: one exchange after the backward)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
 
+    if args.config == 1:                      # the CPU path: no GPU touched
+        if (args.gpus or 1) > 1:
+            raise SystemExit("bench.py --config 1 is the CPU path (one process)")
+        return bench_config1(args)
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -229,8 +323,17 @@ def main():
     cfg = dict(CONFIGS[cfg_id])
     if args.n_rand:
         cfg["N_rand"] = args.n_rand
-    # one process per GPU; modulo only matters for single-GPU gloo rehearsals
-    local_dev = local % max(torch.cuda.device_count(), 1)
+    # one process per GPU.  RCCL needs a device of its own per rank: refuse
+    # before the process group exists (and before any HIP call: the device
+    # count comes from the environment / driver query only) rather than let
+    # ranks share a device.  gloo rehearsals may stack ranks on one GPU.
+    n_dev = torch.cuda.device_count()
+    if world > 1 and args.backend == "nccl" and world > n_dev:
+        print(f"bench.py: --backend nccl with WORLD_SIZE={world} ranks but {n_dev} visible GPU(s): "
+              f"one GPU per rank is required (use --backend gloo for a single-GPU rehearsal)",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+    local_dev = local % max(n_dev, 1)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     if world > 1:
@@ -256,31 +359,17 @@ def main():
         data.bounding_box = tuple(torch.tensor(v) for v in cfg["bbox"])
     tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0, ray_order=args.ray_order)
     tr.skip_dead_rows = not args.dense_table_step
+    tr.dp_chunks = args.dp_chunks
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1
-    # the forward's launch time (reported in "kernels", not in the roofline)
-    # from the warmup steps: each HIP event record idles the device ~5 us, so
-    # the timed steps carry only the two events of the roofline's launch
-    HF.TIMER.reset()
-    HF.TIMER.names = {"render_fwd"}
-    HF.TIMER.enabled = True
     for _ in range(args.warmup):
         tr.step()
-    torch.cuda.synchronize()
-    HF.TIMER.enabled = False
-    fwd_ms = HF.TIMER.mean_ms("render_fwd")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    HF.TIMER.reset()
-    # (world > 1: the owner pass is deferred into the segmented exchange and
-    # timed there as render_bwd_owner; the launch time is the sum)
-    HF.TIMER.names = {"render_bwd", "render_bwd_owner"}
-    # the roofline's launch time from every 4th timed step (>= 5 launches at the
-    # default 20 steps): an event pair idles the device ~10 us per step it brackets
-    HF.TIMER.every = 4 if args.steps >= 20 else 1
-    HF.TIMER.enabled = True
+    # the timed region carries no event records (an event pair idles the
+    # device ~10 us): the kernels' launch times come from the steps after it
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss, mse = tr.step()
@@ -289,13 +378,25 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    HF.TIMER.enabled = False
-    HF.TIMER.every = 1
     HF.L.check_device_faults()                # after the timed region: one blocking read
     t = torch.tensor([dt], device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    # ONE timer for every launch time in the line: HIP events on the launch
+    # stream around the forward and the backward launches (the deferred owner
+    # pass of world > 1 included) of args.kernel_steps further steps, the same
+    # training loop continuing; the committed rocprofv3 kernel-trace summary of
+    # the same command agrees with them (profiles/)
+    HF.TIMER.reset()
+    HF.TIMER.names = {"render_fwd", "render_bwd", "render_bwd_owner"}
+    HF.TIMER.every = 1
+    HF.TIMER.enabled = True
+    for _ in range(args.kernel_steps):
+        tr.step()
+    torch.cuda.synchronize()
+    HF.TIMER.enabled = False
+    fwd_ms = HF.TIMER.mean_ms("render_fwd")
     bwd_ms = HF.TIMER.mean_ms("render_bwd") + HF.TIMER.mean_ms("render_bwd_owner")
     # diagnostic, after the timed region: the host's time to enqueue one step
     # (Python + ctypes; the device runs concurrently) -- at or above
@@ -343,6 +444,8 @@ def main():
                          "bytes_per_ray": BWD_BYTES_PER_RAY, "bytes_per_ray_meaning":
                              "192 unique points x 16 levels x 8 corners x 8 B scatter-added",
                          "launch_ms": round(bwd_ms, 4), "scatter": scatter,
+                         "timer": f"HIP events on the launch stream, {args.kernel_steps} steps after the timed region "
+                                  "(the same timer for every launch time in this line)",
                          # the forward's gather and the whole step, same peak
                          "fwd_gather": {"kernel": "render_fwd_kernel", "bytes_per_ray": FWD_BYTES_PER_RAY,
                                         "launch_ms": round(fwd_ms, 4), "achieved": round(fwd_gbs, 1),
@@ -368,6 +471,21 @@ def main():
                          "parts: 3 parts in the forward (f32-accurate), 2 in the data/weight gradients"),
             "loss": round(float(loss.item()), 6),
         }
+        opt_b = optimizer_bytes(tr) if (world == 1 and tr.fuse_table_step and scatter == "binned") else 0
+        if opt_b:
+            # the fused table RAdam inside the launch (owner pass): p, m, v read
+            # and written on every live row pair -- mandated by the reference's
+            # dense optimizer (radam.py:58-92), reported as its own algorithmic
+            # term beside the scatter-add bytes ("reported separately")
+            alg2 = B * BWD_BYTES_PER_RAY + opt_b
+            gbs2 = alg2 / (bwd_ms * 1e-3) / 1e9 if bwd_ms > 0 else 0.0
+            line["roofline"].update(
+                optimizer_bytes=opt_b, optimizer_bytes_meaning=(
+                    "fused table RAdam: p, m, v (3 x 4 B) read + written per live table parameter "
+                    f"({opt_b // 24:,} of {16 * 2 ** cfg['log2_hashmap_size'] * 2:,})"),
+                with_optimizer={"algorithmic_bytes": alg2, "achieved": round(gbs2, 1),
+                                "frac": round(gbs2 / HBM_PEAK_GBS, 4),
+                                "traffic_ratio": round(traffic / alg2, 3) if traffic else None})
         if scatter == "atomic" and atomics:
             # the binding resource of the atomic scatter: memory-side float-atomic
             # requests (TCC_EA0_ATOMIC, same PMC passes) per second, against

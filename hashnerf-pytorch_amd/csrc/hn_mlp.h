@@ -42,9 +42,6 @@ namespace hn {
 #ifndef HN_SPLIT_B
 #define HN_SPLIT_B 2
 #endif
-#ifndef HN_SPLIT_W   // parts in the fused backward's weight-gradient products
-#define HN_SPLIT_W HN_SPLIT_B
-#endif
 enum : int { R_F0, R_F1, R_F2G, R_F2S, R_F3, R_F4, R_B4, R_B3, R_B2G, R_B2S, R_B1, R_B0, R_N };
 //  F0 sigma_net.0  F1 sigma_net.1  F2G/F2S color_net.0 geo/sh  F3 color_net.1  F4 color_net.2
 //  B4 color_net.2^T  B3 color_net.1^T  B2G/B2S color_net.0^T geo/sh  B1 sigma_net.1^T  B0 sigma_net.0^T
@@ -145,7 +142,9 @@ HN_DEV void relu_mask_or(const f32x16& v, uint32_t& m, int ob) {
 // ReLU as one integer max on the bits (a negative float or -0 is a negative
 // int32): equal to v > 0 ? v : +0 for every non-NaN v, and one v_max_i32
 // where the float form is a v_max_f32 plus the IEEE-mode canonicalisation of
-// its input; a NaN passes through, as in torch.relu.
+// its input.  A NaN with the sign bit clear passes through (as torch.relu
+// propagates NaN); one with the sign bit set is a negative int32 and becomes
+// +0 here.
 HN_DEV void relu16(f32x16& v) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = __int_as_float(max(__float_as_int(v[r]), 0));

@@ -30,28 +30,15 @@
 // SIMD's other waves, whose MLP phases then overlap the gathers' latency.
 // Measured (r04x, config 2, two runs each): render_fwd_kernel 0.2743 ->
 // 0.2673 ms at priority 1 (0.2671 at 2), step 1.005 / 1.000 -> 0.993 / 0.994
-// ms; scheduling only, so every result is unchanged.  0 = off.
-#ifndef HN_FWD_PRIO
-#define HN_FWD_PRIO 1
-#endif
-#if HN_FWD_PRIO
-#define HN_FWD_PRIO_HI() __builtin_amdgcn_s_setprio(HN_FWD_PRIO)
+// ms; scheduling only, so every result is unchanged.
+#define HN_FWD_PRIO_HI() __builtin_amdgcn_s_setprio(1)
 #define HN_FWD_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#else
-#define HN_FWD_PRIO_HI() ((void)0)
-#define HN_FWD_PRIO_LO() ((void)0)
-#endif
-#ifndef HN_ENC_GROUP   // levels per scheduling group of the forward's encode (8 gathers each)
-#define HN_ENC_GROUP 2
-#endif
-#ifndef HN_SC_XROW   // 1: the scatter folds runs that cross its 16-lane rows into one record
-#define HN_SC_XROW 0
-#endif
-#ifndef HN_SC_MERGE_DIAG   // diagnostic builds only: 1 = the merged levels' table inserts skipped (timing)
-#define HN_SC_MERGE_DIAG 0
-#endif
 
 namespace hn {
+
+// levels per scheduling group of the forward's encode (8 gathers each):
+// 1 level 0.2674, 2 levels 0.2666, 4 levels 0.2696 ms (r04z)
+constexpr int kEncGroup = 2;
 
 constexpr int kSc = 64, kNi = 128, kSf = 192;
 constexpr int kFwdWaves = 4;
@@ -207,7 +194,7 @@ HN_DEV void encode_tile(const GridArgs& g, const float* gsl, const float* __rest
     encode_level_off(table, l << g.log2T, v, f0, f1);
     feat[2 * m] = f0;
     feat[2 * m + 1] = f1;
-    if ((m & (HN_ENC_GROUP - 1)) == HN_ENC_GROUP - 1) __builtin_amdgcn_sched_barrier(0);   // <= 8 x HN_ENC_GROUP gathers in flight
+    if ((m & (kEncGroup - 1)) == kEncGroup - 1) __builtin_amdgcn_sched_barrier(0);   // <= 8 x kEncGroup gathers in flight
   }
 }
 
@@ -1368,10 +1355,7 @@ constexpr size_t kDcRay = (size_t)kSc * 32;
 // read is latency bound otherwise), LDS combine in a fixed order, so the sums
 // are deterministic given the slabs.
 constexpr int kSlabGroups = 16;
-#ifndef HN_SLAB_ILP   // slab loads in flight per thread (a power of 2)
-#define HN_SLAB_ILP 8
-#endif
-constexpr int kSlabIlp = HN_SLAB_ILP;
+constexpr int kSlabIlp = 8;   // slab loads in flight per thread (a power of 2)
 // One slab-reduce block's 64 elements (vblock): the arithmetic of every
 // element is fixed (the group partials, then the pairwise combines), so the
 // sums are the same whichever kernel runs it (slab_reduce_kernel, or the
@@ -1481,16 +1465,29 @@ constexpr int kStMinLog2C = 3;                          // fewer than 8 records 
 // 64-bit fixed point, 36 B per slot
 constexpr uint32_t kMhEmpty = 0xffffffffu;   // never an entry word (bits 26-27 are zero)
 static_assert((1 << 11) * 36 <= kStPool * 20, "a 2,048-slot merge table fits the staging pool");
-constexpr size_t kScStaticLds = 10 * 1024;   // the kernel's static LDS (checked at launch)
 constexpr size_t kLdsMax = 160 * 1024;
-// dynamic LDS of scatter_bins_kernel: the counters, then max(pool, table)
-static int sc_mh_log2(int nbins) {
-  const size_t cnt = (size_t)((nbins + 3) & ~3) * 4;
-  return kScStaticLds + cnt + ((size_t)36 << 12) <= kLdsMax ? 12 : 11;
+__global__ void scatter_bins_kernel(ScK k);
+// the kernel's static LDS, read once from the code object (a
+// constant here would silently go stale if the static arrays grow)
+static size_t sc_static_lds() {
+  static size_t v = 0;
+  if (!v) {
+    hipFuncAttributes at{};
+    v = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&scatter_bins_kernel)) == hipSuccess
+            ? at.sharedSizeBytes : (size_t)16 * 1024;
+  }
+  return v;
 }
-static size_t sc_lds_bytes(int nbins) {
+// dynamic LDS of scatter_bins_kernel: the counters, then max(pool, table);
+// the merge table grows to 4,096 slots only when levels are merged and the
+// whole allocation still fits the CU's LDS
+static int sc_mh_log2(int nbins, int merge_levels) {
+  const size_t cnt = (size_t)((nbins + 3) & ~3) * 4;
+  return merge_levels != 0 && sc_static_lds() + cnt + ((size_t)36 << 12) <= kLdsMax ? 12 : 11;
+}
+static size_t sc_lds_bytes(int nbins, int mh_log2) {
   const size_t cnt = (size_t)((nbins + 3) & ~3) * 4, pool = (size_t)kStPool * 20;
-  const size_t tab = (size_t)36 << sc_mh_log2(nbins);
+  const size_t tab = (size_t)36 << mh_log2;
   return cnt + (pool > tab ? pool : tab);
 }
 struct StPhase {
@@ -1671,48 +1668,9 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
       v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
       seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
-#if !HN_SC_XROW
       vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
-#endif
     }
-#if HN_SC_XROW
-    // Runs that continue across the 16-lane rows: row r's first lane (a head
-    // only because rows are summed separately) is folded into the last run
-    // head of row r - 1, for r = 3, 2, 1 in that order (a run spanning several
-    // rows ends in its first row's head); a fixed order of fp32 adds, so the
-    // records stay a function of the unit's samples alone
-    {
-      uint64_t he = hb;
-#pragma unroll
-      for (int r = 3; r >= 1; --r) {
-        const int l0 = 16 * r;
-        const bool cont = __builtin_amdgcn_readlane((int)cx, l0) == __builtin_amdgcn_readlane((int)cx, l0 - 1) &&
-                          __builtin_amdgcn_readlane((int)y0, l0) == __builtin_amdgcn_readlane((int)y0, l0 - 1) &&
-                          __builtin_amdgcn_readlane((int)z0, l0) == __builtin_amdgcn_readlane((int)z0, l0 - 1);
-        if (cont) {   // wave-uniform
-          const uint32_t rm = (uint32_t)(he >> (l0 - 16)) & 0xffffu;   // row r - 1's heads (bit 0 always set)
-          const int t = l0 - 16 + 31 - __builtin_clz(rm);
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[c][e]), l0));
-              v[c][e] = lane == t ? v[c][e] + s : v[c][e];
-            }
-          he &= ~(1ull << l0);
-        }
-      }
-      head = ((he >> lane) & 1ull) != 0ull;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
-    }
-#endif
     if (mode == kMerged) {
-#if HN_SC_MERGE_DIAG
-      if (head && __float_as_uint(v[0][0]) == 0x7fc00001u) mh_fail = 1u;   // (keeps v live)
-      return;
-#endif
       if (head) {
         // the 4 corner rows' slots: their first probes in flight together (a
         // plain read: most inserts find their word already there, and
@@ -2505,10 +2463,7 @@ constexpr int kSliceF4 = 4;   // float4s of a 2^13-entry slice per thread (2 x 2
 // VGPR spills): vmcnt waits are in order, so an earlier issue only moves the
 // wait to the first records.
 static_assert(kSliceF4 * kBinThreads * 4 >= (2 << 13), "bins are at most 2^13 entries (bin_geom)");
-#ifndef HN_BR_DEPTH   // records per thread and fetch group (two groups in flight)
-#define HN_BR_DEPTH 4
-#endif
-constexpr int kBrDepth = HN_BR_DEPTH;
+constexpr int kBrDepth = 4;   // records per thread and fetch group (two groups in flight)
 constexpr int kBrChunks = 8192;   // table entries (16 KiB of LDS): bins of up to 512 K records
 
 
@@ -3147,8 +3102,10 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.df = a->d_fine;
     sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
     sk.merge_levels = merge_levels(cfg);
-    sk.mh_log2 = sc_mh_log2(sk.nbins);
-    hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), sc_lds_bytes(sk.nbins), s, sk);
+    sk.mh_log2 = sc_mh_log2(sk.nbins, sk.merge_levels);
+    const size_t sc_lds = sc_lds_bytes(sk.nbins, sk.mh_log2);
+    if (sc_lds + sc_static_lds() > kLdsMax) return HN_E_SHAPE;   // bins beyond the LDS counters' room
+    hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), sc_lds, s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
   if (mode != kModeAtomic) {

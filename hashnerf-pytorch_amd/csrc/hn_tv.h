@@ -33,10 +33,7 @@ HN_DEV int tv_level(const TvK& k, const int32_t* off, int b) {
 
 // vertices per forward thread: fewer blocks, so fewer same-address atomics
 // on the 16 level sums
-#ifndef HN_TV_FWD_V
-#define HN_TV_FWD_V 4
-#endif
-constexpr int kTvFwdV = HN_TV_FWD_V;
+constexpr int kTvFwdV = 4;
 
 HN_DEV float tv_val(const TvK& k, int l, uint32_t x, uint32_t y, uint32_t z, int f) {
   const uint32_t mask = (1u << k.log2T) - 1u;

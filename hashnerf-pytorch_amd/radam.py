@@ -193,4 +193,12 @@ class RAdam(Optimizer):
                 new_ids.append(nxt)
                 nxt += 1
             groups.append({**gsd, "params": new_ids})
-        return super().load_state_dict({"state": state, "param_groups": groups})
+        out = super().load_state_dict({"state": state, "param_groups": groups})
+        # data-parallel sharded table step: the table's moments live on the
+        # ranks' shards, seeded once from optimizer.state; the loaded moments
+        # must reach the shards too, or training would silently continue on the
+        # old ones
+        xchg = getattr(self, "sharded_state", None)
+        if xchg is not None:
+            xchg.load_state(self.state.get(xchg.table))
+        return out

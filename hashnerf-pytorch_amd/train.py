@@ -127,21 +127,28 @@ def allreduce_grads(table, mlp_params, group=None, live=None):
 
 
 class Collectives:
-    """The two collectives of the sharded table step with RCCL's calling
-    convention: ``reduce_scatter(out, inp)`` = ``reduce_scatter_tensor``
-    (SUM; ``out`` is this rank's 1/world slice of ``inp``'s sum) and
-    ``all_gather(out, inp)`` = ``all_gather_into_tensor`` (``inp`` may be
-    ``out``'s own slice: in place).  On gloo, which has neither, each is
-    emulated INTO THE SAME out tensor (all-reduce + copy of the rank's slice;
-    a list all-gather over ``out``'s views), so the offsets, views and
-    out-tensors that the RCCL run uses are exactly what a gloo test runs --
-    only the transport differs (``inp`` of a gloo reduce_scatter is left
-    holding the full sum; the RCCL call leaves it untouched, and the step
-    never reads it again)."""
+    """The two collectives of the sharded table step: ``reduce_scatter(out,
+    inp)`` = ``reduce_scatter_tensor`` (SUM; ``out`` is this rank's 1/world
+    slice of ``inp``'s sum) and ``all_gather(out, inp)`` =
+    ``all_gather_into_tensor`` (``inp`` may be ``out``'s own slice: in
+    place).  These production calls run on RCCL and on gloo with host
+    tensors (torch 2.10's gloo implements both, async reduce-scatter and the
+    in-place all-gather included), so the CPU gloo tests execute exactly the
+    calls an RCCL run makes.
 
-    def __init__(self, rank, world, group=None, emulate=None):
+    ``emulate=True`` replaces each call by an emulation INTO THE SAME out
+    tensor (all-reduce + copy of the rank's slice; a list all-gather over
+    ``out``'s views).  It is the default only for gloo on device tensors
+    (the GPU DP tests run two ranks of one GPU over gloo, whose device-tensor
+    support covers all_reduce / all_gather); the gloo CPU test holds the two
+    forms bitwise equal (tests/test_dp_gloo.py)."""
+
+    def __init__(self, rank, world, group=None, emulate=None, device=None):
         self.rank, self.world, self.group = rank, world, group
-        self.emulate = dist.get_backend(group) == "gloo" if emulate is None else emulate
+        if emulate is None:
+            dev = torch.device(device) if device is not None else torch.device("cpu")
+            emulate = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+        self.emulate = emulate
 
     def reduce_scatter(self, out, inp, async_op=False):
         """Returns the RCCL work handle with async_op (None under gloo, whose
@@ -205,10 +212,11 @@ class ShardedTableStep:
     gather_state(): RAdam.state_dict() refuses to write a checkpoint while the
     optimizer's full-size copy is stale (Trainer.sync_optimizer_state)."""
 
-    def __init__(self, table, live, rank, world, group=None, state=None, stepper=None, bins=None, n_chunks=4):
+    def __init__(self, table, live, rank, world, group=None, state=None, stepper=None, bins=None, n_chunks=4,
+                 emulate=None):
         L_, R, F_ = table.shape
         self.table, self.rank, self.world, self.group = table, rank, world, group
-        self.coll = Collectives(rank, world, group)
+        self.coll = Collectives(rank, world, group, emulate=emulate, device=table.device)
         self.stepper = HF.radam_step if stepper is None else stepper
         self.full = L_ * R * F_
         n_lv, rows = live if live is not None else (0, None)
@@ -234,10 +242,20 @@ class ShardedTableStep:
         self.m = torch.zeros(self.s, dtype=torch.float32, device=dev)
         self.v = torch.zeros(self.s, dtype=torch.float32, device=dev)
         self._gath = None   # rank-major all-gather buffer (segmented exchange)
+        self.load_state(state)
+
+    @torch.no_grad()
+    def load_state(self, state):
+        """(Re)seed this rank's moment shards from the table's full-size
+        optimizer state (exp_avg / exp_avg_sq); zeros without one.  Called at
+        construction and by RAdam.load_state_dict (a checkpoint loaded after
+        the sharded step began)."""
         if state is not None and "exp_avg" in state:
-            with torch.no_grad():
-                self.m.copy_(self._shard_of(state["exp_avg"]))
-                self.v.copy_(self._shard_of(state["exp_avg_sq"]))
+            self.m.copy_(self._shard_of(state["exp_avg"]))
+            self.v.copy_(self._shard_of(state["exp_avg_sq"]))
+        else:
+            self.m.zero_()
+            self.v.zero_()
         self.stale = False
 
     def _segments(self, bins, n_chunks):
@@ -540,8 +558,11 @@ class Trainer:
         self.dp_sharded = True
         # ... in this many bin-aligned segments, each exchanged as soon as the
         # backward's owner pass has formed it (1: one exchange after the whole
-        # backward)
-        self.dp_chunks = 4
+        # backward).  1 by default: the segmented form's RCCL overlap (segment
+        # k's reduce-scatter on RCCL's stream while the owner pass forms
+        # segment k+1) has run only on gloo so far; the GPU DP
+        # tests and bench.py --dp-chunks select it
+        self.dp_chunks = 1
         self._xchg = None
         self._owner_st = None
 
@@ -664,6 +685,11 @@ class Trainer:
         table = self.embed_fn.table
         # world > 1 (explicit mode): the table's exchange + RAdam step sharded over
         # the ranks (ShardedTableStep); the backward writes into its buffer
+        if self._xchg is not None and self._xchg.stale:
+            # a rebuilt exchange seeds its shards from optimizer.state, which is
+            # out of date while the previous exchange's moments are newer
+            raise RuntimeError("Trainer: the sharded table moments are newer than optimizer.state; "
+                               "call sync_optimizer_state() on every rank before rebuilding the step")
         self._xchg = None
         if self.world > 1 and self.dp_sharded:
             # the moments continue from the optimizer's (a resumed run's
@@ -713,6 +739,8 @@ class Trainer:
             batch = self.draw_batch(i)
         rays, target, t_rand, u = batch["rays"], batch["target"], batch["t_rand"], batch["u"]
         table = self.embed_fn.table
+        if rays.shape[0] == 0:
+            return self._empty_rank_grads(batch)
         out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
         tv = mv = cubes = None
         if batch["tv"] is not None:
@@ -746,6 +774,30 @@ class Trainer:
                           owner_defer=defer)
             self._owner_st = st if defer else None
             table.grad = self._gtable
+        for p, g in zip(self._ws, self._gws):
+            p.grad = g
+        return lo[0], lo[1]
+
+    def _empty_rank_grads(self, batch):
+        """A rank that drew no rays this step (world > 1, use_batching: the
+        short last batch of an epoch holds fewer positions than ranks,
+        run_nerf.py:551-555) still joins the exchange: its gradient is the TV
+        term's alone (rank 0) or zero, its MSE / entropy terms empty."""
+        table = self.embed_fn.table
+        if self.world == 1:
+            raise RuntimeError("Trainer: an empty batch on a single rank")
+        self._owner_st = None
+        self._gtable.zero_()
+        lo = torch.zeros(2, device=self.device)
+        if batch["tv"] is not None:
+            cubes, mv0 = batch["tv"]
+            tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
+            w = self.args.tv_loss_weight
+            lo[0] = w * tv.sum()
+            HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, torch.full_like(tv, w), self._gtable)
+        table.grad = self._gtable
+        for g in self._gws:
+            g.zero_()
         for p, g in zip(self._ws, self._gws):
             p.grad = g
         return lo[0], lo[1]

@@ -64,6 +64,10 @@ def train(out_path, sharded, steps, resume_at=0):
     args = default_args(N_rand=256, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=4, sparse_loss_weight=1e-3)
     tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)
     tr.dp_sharded = sharded
+    # the uninterrupted sharded run exchanges in 4 bin-aligned segments (each
+    # reduce-scattered right after the owner pass forms it); the resumed run
+    # in one (Trainer's default)
+    tr.dp_chunks = 4 if not resume_at else 1
     for k in range(steps):
         if resume_at and k == resume_at:
             tr.sync_optimizer_state()
@@ -84,8 +88,45 @@ def train(out_path, sharded, steps, resume_at=0):
     dist.destroy_process_group()
 
 
+def train_pool(out_path, steps, emulate):
+    """use_batching (the global shuffled ray pool, run_nerf.py:505-555) on a
+    pool whose epoch ends in a batch of ONE position for two ranks: rank 1
+    draws no rays that step and must still join the exchange.
+    emulate: "1" = gloo's emulated collectives, "0" = the production
+    reduce_scatter_tensor / all_gather_into_tensor calls on device tensors."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    import hn_loader
+    hn_loader.load()
+    from hashnerf_pytorch_amd.train import ShardedTableStep, SyntheticBlender, Trainer, default_args
+    dev = torch.device("cuda", 0)
+    # 1 image of 7 x 19 = 133 rays = 2 x 66 + 1: every second step's batch is 1 ray
+    data = SyntheticBlender(7, 19, 1, dev, seed=0)
+    args = default_args(N_rand=66, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=10 ** 6,
+                        sparse_loss_weight=1e-3, no_batching=False)
+    tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)
+    if emulate is not None:
+        tr._fused_setup()
+        tr._xchg.coll.emulate = emulate
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    from hashnerf_pytorch_amd import _lib
+    _lib.check_device_faults()
+    tr.sync_optimizer_state()
+    if rank == 0:
+        t = tr.embed_fn.table
+        torch.save({"table": t.detach().cpu(), "finite": bool(torch.isfinite(t).all()), "step": tr.global_step},
+                   out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "train":
+    if sys.argv[1] == "train_pool":
+        em = {"-": None, "1": True, "0": False}[sys.argv[4]]
+        train_pool(sys.argv[2], int(sys.argv[3]), em)
+    elif sys.argv[1] == "train":
         train(sys.argv[2], sys.argv[3] == "1", int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 0)
     else:
         main(sys.argv[1], sys.argv[2])

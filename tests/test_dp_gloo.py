@@ -226,52 +226,62 @@ def _sharded_worker(rank, world, port, out_path, n_chunks=1):
             out.append(g)
         return out
 
-    # sharded: RCCL's call sequence, the collectives emulated on gloo
-    table = torch.nn.Parameter(p0.clone())
-    # n_chunks > 1: bins of 16 rows (32 floats), the exchange in bin-aligned
-    # segments, each segment's gradient formed just before its exchange (the
-    # trainer's deferred owner pass) over a gradient buffer holding NaN
-    bins = (L_ * R // 16, 4) if n_chunks > 1 else None
-    xs = ShardedTableStep(table, live, rank, world, state={"exp_avg": m0, "exp_avg_sq": v0},
-                          stepper=_toy_step, bins=bins, n_chunks=n_chunks)
-    assert xs.coll.emulate
-    assert len(xs.segs) == (3 if n_chunks > 1 else 1)
-    for step in range(3):
-        g = grads(step)[rank]
-        if n_chunks > 1:
-            xs.grad_view().fill_(float("nan"))
+    def run(emulate):
+        # n_chunks > 1: bins of 16 rows (32 floats), the exchange in bin-aligned
+        # segments, each segment's gradient formed just before its exchange (the
+        # trainer's deferred owner pass) over a gradient buffer holding NaN
+        table = torch.nn.Parameter(p0.clone())
+        bins = (L_ * R // 16, 4) if n_chunks > 1 else None
+        xs = ShardedTableStep(table, live, rank, world, state={"exp_avg": m0, "exp_avg_sq": v0},
+                              stepper=_toy_step, bins=bins, n_chunks=n_chunks, emulate=emulate)
+        # default on host tensors: the production calls (reduce_scatter_tensor
+        # with async_op, in-place all_gather_into_tensor), as an RCCL run makes them
+        assert xs.coll.emulate == bool(emulate)
+        assert len(xs.segs) == (3 if n_chunks > 1 else 1)
+        for step in range(3):
+            g = grads(step)[rank]
+            if n_chunks > 1:
+                xs.grad_view().fill_(float("nan"))
 
-            def produce(k, g=g):
-                lo, hi = xs.seg_bins[k]
-                xs.grad_view().view(-1)[lo * 32:hi * 32] = g.reshape(-1)[lo * 32:hi * 32]
-            xs.step(c, produce=produce)
-        else:
-            xs.grad_view().copy_(g)
-            xs.step(c)
-    assert xs.stale
-    m, v = xs.gather_state()
-    assert not xs.stale
+                def produce(k, g=g):
+                    lo, hi = xs.seg_bins[k]
+                    xs.grad_view().view(-1)[lo * 32:hi * 32] = g.reshape(-1)[lo * 32:hi * 32]
+                xs.step(c, produce=produce)
+            else:
+                xs.grad_view().copy_(g)
+                xs.step(c)
+        assert xs.stale
+        m, v = xs.gather_state()
+        assert not xs.stale
+        return table.detach().clone(), m, v
+
+    p_n, m_n, v_n = run(None)     # production collectives
+    p_e, m_e, v_e = run(True)     # the emulation (gloo on device tensors)
     # reference: the summed gradient, the dense update over the whole table
     pr, mr, vr = p0.clone(), m0.clone(), v0.clone()
     for step in range(3):
         _toy_step([(pr, sum(grads(step)), mr, vr, c)])
     if rank == 0:
-        torch.save({"p": table.detach().clone(), "m": m, "v": v, "pr": pr, "mr": mr, "vr": vr}, out_path)
+        torch.save({"p": p_n, "m": m_n, "v": v_n, "pe": p_e, "me": m_e, "ve": v_e,
+                    "pr": pr, "mr": mr, "vr": vr}, out_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("n_chunks", [1, 3])
 def test_sharded_table_step_matches_dense(tmp_path, n_chunks):
-    """train.ShardedTableStep through train.Collectives (gloo emulating
-    reduce_scatter_tensor / all_gather_into_tensor into the RCCL call's own
-    out-tensors and offsets): 3 steps from loaded moments (a resumed run) leave
+    """train.ShardedTableStep through train.Collectives: the production calls
+    (reduce_scatter_tensor with async_op, in-place all_gather_into_tensor) on
+    gloo, and the emulation into the same out-tensors and offsets, give
+    bitwise the same result; 3 steps from loaded moments (a resumed run) leave
     the table and the gathered moments equal to the summed-gradient dense
     update; the dead coarse rows stay untouched.  n_chunks=3: the same in
     bin-aligned segments, each formed (produce) right before its exchange."""
     port = _free_port()
     mp.spawn(_sharded_worker, args=(2, port, str(tmp_path / "sh.pt"), n_chunks), nprocs=2, join=True)
     got = torch.load(tmp_path / "sh.pt", weights_only=True)
+    for k in ("p", "m", "v"):   # production calls and emulation: bitwise the same step
+        assert torch.equal(got[k], got[k + "e"]), k
     torch.testing.assert_close(got["p"], got["pr"], rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(got["m"], got["mr"], rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(got["v"], got["vr"], rtol=1e-6, atol=1e-7)
@@ -292,3 +302,47 @@ def test_sharded_state_dict_refuses_stale_moments():
         opt.state_dict()
     opt.sharded_state.stale = False
     opt.state_dict()
+
+
+def _load_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    import hn_loader
+    hn = hn_loader.load()
+    from hashnerf_pytorch_amd.train import ShardedTableStep
+    L_, R, F_ = 2, 32, 2
+    g0 = torch.Generator().manual_seed(5)
+    table = torch.nn.Parameter(torch.randn(L_, R, F_, generator=g0))
+    opt = hn.RAdam([table], lr=0.1)
+    xs = ShardedTableStep(table, None, rank, world, stepper=_toy_step)
+    opt.sharded_state = xs
+    xs.grad_view().copy_(torch.randn(L_, R, F_, generator=g0))
+    xs.step({"beta1": 0.9, "beta2": 0.99, "lr": 0.05})
+    assert xs.stale
+    # a checkpoint loaded after the first sharded step: its moments must reach
+    # the shards (and the stale flag clear), not stay in optimizer.state only
+    m1, v1 = torch.randn(L_, R, F_, generator=g0), torch.rand(L_, R, F_, generator=g0)
+    sd = {"state": {0: {"step": 7, "exp_avg": m1, "exp_avg_sq": v1}},
+          "param_groups": [{**{k: v for k, v in opt.param_groups[0].items() if k != "params"}, "params": [0]}]}
+    opt.load_state_dict(sd)
+    assert not xs.stale
+    m, v = xs.gather_state()
+    ok = torch.equal(m, m1) and torch.equal(v, v1)
+    # a rebuilt trainer setup refuses to seed shards from a stale optimizer copy
+    xs.stale = True
+    if rank == 0:
+        torch.save({"ok": ok, "shard_m": xs.m.clone(), "want": xs._shard_of(m1)}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_moments_follow_load_state_dict(tmp_path):
+    """RAdam.load_state_dict after the sharded table step began
+    re-seeds the ranks' moment shards from the loaded exp_avg / exp_avg_sq."""
+    port = _free_port()
+    mp.spawn(_load_worker, args=(2, port, str(tmp_path / "ld.pt")), nprocs=2, join=True)
+    got = torch.load(tmp_path / "ld.pt", weights_only=True)
+    assert got["ok"]
+    assert torch.equal(got["shard_m"], got["want"])

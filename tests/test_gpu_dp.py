@@ -84,6 +84,8 @@ def test_dp_sharded_table_step_equals_allreduce(hn, tmp_path):
     the same kernel).  The collectives run RCCL's calls (reduce_scatter_tensor
     into the shard, in-place all_gather_into_tensor into the parameter
     buffer), emulated on gloo into the same out-tensors (train.Collectives).
+    The first sharded run exchanges in 4 bin-aligned segments (deferred
+    owner pass per segment), the resumed one in a single exchange.
     The second sharded run resumes after 7 steps: the moments are gathered
     into the optimizer, the exchange is rebuilt from them, and the run ends
     bitwise where the uninterrupted all-reduce run does (the moments must
@@ -102,6 +104,37 @@ def test_dp_sharded_table_step_equals_allreduce(hn, tmp_path):
         assert torch.count_nonzero(a["m"]) > 0
         for x, y in zip(a["mlp"], b["mlp"]):
             assert torch.equal(x, y), name
+
+
+def test_dp_empty_rank_batch(hn, tmp_path):
+    """use_batching with a pool of 133 rays, N_rand 66, two ranks: every
+    second step's global batch is the epoch's last position alone, so rank 1
+    draws no rays; it joins the sharded exchange with a zero (TV-free)
+    gradient instead of failing inside the owner pass while rank 0 waits in
+    the reduce-scatter.  Six steps (three empty-rank steps)."""
+    out = str(tmp_path / "pool.pt")
+    _launch(["train_pool", out, "6", "-"])
+    got = torch.load(out, weights_only=True)
+    assert got["step"] == 6 and got["finite"]
+
+
+def test_dp_device_collectives_production_calls(hn, tmp_path):
+    """The sharded exchange on device tensors through the production calls
+    (reduce_scatter_tensor with async_op, in-place all_gather_into_tensor) on
+    gloo, against the emulation the GPU tests use by default: the same table
+    after six steps (incl. the empty-rank steps above).  Skipped where this
+    gloo build does not implement the calls for device tensors."""
+    res = {}
+    for em in ("1", "0"):
+        out = str(tmp_path / f"pool_{em}.pt")
+        try:
+            _launch(["train_pool", out, "6", em])
+        except AssertionError:
+            if em == "0":
+                pytest.skip("gloo: reduce_scatter_tensor / all_gather_into_tensor unsupported on device tensors")
+            raise
+        res[em] = torch.load(out, weights_only=True)
+    assert torch.equal(res["0"]["table"], res["1"]["table"])
 
 
 @pytest.mark.parametrize("B,T,HW,i", [(512, 14, 64, 1), (16384, 19, 200, 501)],
