@@ -145,10 +145,16 @@ class Collectives:
 
     def __init__(self, rank, world, group=None, emulate=None, device=None):
         self.rank, self.world, self.group = rank, world, group
-        if emulate is None:
-            dev = torch.device(device) if device is not None else torch.device("cpu")
-            emulate = dist.get_backend(group) == "gloo" and dev.type != "cpu"
-        self.emulate = emulate
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        gloo_dev = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+        self.emulate = gloo_dev if emulate is None else emulate
+        # gloo's own calls on device tensors (test_gpu_dp): the device is
+        # drained before each, so gloo's host staging reads finished inputs
+        self.drain = gloo_dev and not self.emulate
+
+    def _ready(self):
+        if self.drain:
+            torch.cuda.synchronize()
 
     def reduce_scatter(self, out, inp, async_op=False):
         """Returns the RCCL work handle with async_op (None under gloo, whose
@@ -160,6 +166,7 @@ class Collectives:
             dist.all_reduce(inp, group=self.group)
             out.copy_(inp[self.rank * n:(self.rank + 1) * n])
             return None
+        self._ready()
         return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
 
     def all_gather(self, out, inp):
@@ -169,6 +176,7 @@ class Collectives:
         if self.emulate:
             dist.all_gather(list(out.chunk(self.world)), inp.clone(), group=self.group)
         else:
+            self._ready()
             dist.all_gather_into_tensor(out, inp, group=self.group)
 
 

@@ -108,6 +108,7 @@ def train_pool(out_path, steps, emulate):
     if emulate is not None:
         tr._fused_setup()
         tr._xchg.coll.emulate = emulate
+        tr._xchg.coll.drain = not emulate     # gloo's device calls read host-staged inputs
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()

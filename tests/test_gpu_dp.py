@@ -122,8 +122,12 @@ def test_dp_device_collectives_production_calls(hn, tmp_path):
     """The sharded exchange on device tensors through the production calls
     (reduce_scatter_tensor with async_op, in-place all_gather_into_tensor) on
     gloo, against the emulation the GPU tests use by default: the same table
-    after six steps (incl. the empty-rank steps above).  Skipped where this
-    gloo build does not implement the calls for device tensors."""
+    after six steps (incl. the empty-rank steps above).  gloo stages device
+    tensors through the host without ordering itself after the compute
+    stream (without a drain the table differed, r05a), so Collectives drains
+    the device before each gloo call on device tensors; RCCL orders its
+    stream after the caller's.  Skipped where this gloo build does not
+    implement the calls for device tensors."""
     res = {}
     for em in ("1", "0"):
         out = str(tmp_path / f"pool_{em}.pt")
