@@ -139,22 +139,15 @@ class Collectives:
     ``emulate=True`` replaces each call by an emulation INTO THE SAME out
     tensor (all-reduce + copy of the rank's slice; a list all-gather over
     ``out``'s views).  It is the default only for gloo on device tensors
-    (the GPU DP tests run two ranks of one GPU over gloo, whose device-tensor
-    support covers all_reduce / all_gather); the gloo CPU test holds the two
-    forms bitwise equal (tests/test_dp_gloo.py)."""
+    (the GPU DP tests run two ranks of one GPU over gloo); the gloo tests hold
+    the two forms bitwise equal on host tensors (tests/test_dp_gloo.py) and
+    on device tensors (tests/test_gpu_dp.py)."""
 
     def __init__(self, rank, world, group=None, emulate=None, device=None):
         self.rank, self.world, self.group = rank, world, group
         dev = torch.device(device) if device is not None else torch.device("cpu")
         gloo_dev = dist.get_backend(group) == "gloo" and dev.type != "cpu"
         self.emulate = gloo_dev if emulate is None else emulate
-        # gloo's own calls on device tensors (test_gpu_dp): the device is
-        # drained before each, so gloo's host staging reads finished inputs
-        self.drain = gloo_dev and not self.emulate
-
-    def _ready(self):
-        if self.drain:
-            torch.cuda.synchronize()
 
     def reduce_scatter(self, out, inp, async_op=False):
         """Returns the RCCL work handle with async_op (None under gloo, whose
@@ -166,7 +159,6 @@ class Collectives:
             dist.all_reduce(inp, group=self.group)
             out.copy_(inp[self.rank * n:(self.rank + 1) * n])
             return None
-        self._ready()
         return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
 
     def all_gather(self, out, inp):
@@ -176,7 +168,6 @@ class Collectives:
         if self.emulate:
             dist.all_gather(list(out.chunk(self.world)), inp.clone(), group=self.group)
         else:
-            self._ready()
             dist.all_gather_into_tensor(out, inp, group=self.group)
 
 

@@ -88,7 +88,7 @@ def train(out_path, sharded, steps, resume_at=0):
     dist.destroy_process_group()
 
 
-def train_pool(out_path, steps, emulate):
+def train_pool(out_path, steps, emulate, tv=True):
     """use_batching (the global shuffled ray pool, run_nerf.py:505-555) on a
     pool whose epoch ends in a batch of ONE position for two ranks: rank 1
     draws no rays that step and must still join the exchange.
@@ -100,15 +100,17 @@ def train_pool(out_path, steps, emulate):
     hn_loader.load()
     from hashnerf_pytorch_amd.train import ShardedTableStep, SyntheticBlender, Trainer, default_args
     dev = torch.device("cuda", 0)
-    # 1 image of 7 x 19 = 133 rays = 2 x 66 + 1: every second step's batch is 1 ray
+    # 1 image of 7 x 19 = 133 rays = 2 x 66 + 1: every second step's batch is
+    # 1 ray (rank 0 draws none, rank 1 the one: train._pool_draw's split)
     data = SyntheticBlender(7, 19, 1, dev, seed=0)
-    args = default_args(N_rand=66, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=10 ** 6,
+    # (tv=False: the empty rank's TV backward is the float-atomic hn_tv_bwd,
+    # whose sums are not bitwise reproducible; comparisons run without TV)
+    args = default_args(N_rand=66, log2_hashmap_size=14, tv_loss_weight=1e-4 if tv else 0.0, tv_until=10 ** 6,
                         sparse_loss_weight=1e-3, no_batching=False)
     tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)
     if emulate is not None:
         tr._fused_setup()
         tr._xchg.coll.emulate = emulate
-        tr._xchg.coll.drain = not emulate     # gloo's device calls read host-staged inputs
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
@@ -123,10 +125,33 @@ def train_pool(out_path, steps, emulate):
     dist.destroy_process_group()
 
 
+def probe(out_path):
+    """gloo's reduce_scatter_tensor (async) and all_gather_into_tensor on
+    device tensors against their definition: rank 0 saves what it got."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    dev = torch.device("cuda", 0)
+    inp = torch.arange(4 * world, dtype=torch.float32, device=dev) + 100 * rank
+    out = torch.full((4,), -1.0, device=dev)
+    dist.reduce_scatter_tensor(out, inp, async_op=True).wait()
+    want = sum(torch.arange(4 * world, dtype=torch.float32) + 100 * r for r in range(world))[4 * rank:4 * rank + 4]
+    g = torch.full((4 * world,), -1.0, device=dev)
+    dist.all_gather_into_tensor(g, out)
+    torch.cuda.synchronize()
+    if rank == 0:
+        torch.save({"rs": out.cpu(), "rs_want": want, "ag": g.cpu(),
+                    "ag_want": sum(torch.arange(4 * world, dtype=torch.float32) + 100 * r for r in range(world))},
+                   out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "train_pool":
+    if sys.argv[1] == "probe":
+        probe(sys.argv[2])
+    elif sys.argv[1] == "train_pool":
         em = {"-": None, "1": True, "0": False}[sys.argv[4]]
-        train_pool(sys.argv[2], int(sys.argv[3]), em)
+        train_pool(sys.argv[2], int(sys.argv[3]), em, len(sys.argv) <= 5 or sys.argv[5] == "1")
     elif sys.argv[1] == "train":
         train(sys.argv[2], sys.argv[3] == "1", int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 0)
     else:
