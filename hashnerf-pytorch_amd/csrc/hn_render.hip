@@ -1491,17 +1491,25 @@ static size_t sc_lds_bytes(int nbins, int mh_log2) {
   return cnt + (pool > tab ? pool : tab);
 }
 struct StPhase {
-  int b0, log2c;   // first bin of the level, log2 pool records per bin (< kStMinLog2C: direct)
-  int nbl;         // bins of the level
+  int b0, log2c;   // first bin of the phase's levels, log2 pool records per bin (< kStMinLog2C: direct)
+  int nbl;         // bins of the phase's levels
 };
-HN_DEV StPhase st_phase(int l, int log2T, int shift) {
+// a staging phase: levels l .. l + 2^lg2n - 1 (their bins are consecutive;
+// several levels per phase only where every level owns whole bins)
+HN_DEV StPhase st_phase(int l, int log2T, int shift, int lg2n = 0) {
   StPhase ph;
   ph.b0 = (int)(((uint32_t)l << log2T) >> shift);
   const int lg = log2T > shift ? log2T - shift : 0;
-  ph.nbl = 1 << lg;
-  ph.log2c = kStLog2 - lg;
+  ph.nbl = 1 << (lg + lg2n);
+  ph.log2c = kStLog2 - lg - lg2n;
   return ph;
 }
+#ifndef HN_SC_PF   // the next level's grads loaded while a level runs
+#define HN_SC_PF 1
+#endif
+#ifndef HN_SC_LPP   // log2 levels per staging phase (one block barrier pair per phase)
+#define HN_SC_LPP 0
+#endif
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // dynamic LDS: the bins' record counters, then the staging pool / merge
@@ -1554,14 +1562,12 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // first staged slot of each bin of level l (the bins' counts so far, capped)
   // (stfl alternates between phases: par = the phase's parity)
   int par = 0;
-  auto st_init = [&](int l, int pr) {
-    const StPhase ph = st_phase(l, log2T, sh);
+  auto st_init = [&](const StPhase& ph, int pr) {
     if (ph.log2c < kStMinLog2C) return;
     for (int i = threadIdx.x; i < ph.nbl; i += blockDim.x) stfl[pr][i] = min(bcnt[ph.b0 + i], bw.cap);
   };
   // the pool's records of level l to their regions, in slot order
-  auto st_flush = [&](int l) {
-    const StPhase ph = st_phase(l, log2T, sh);
+  auto st_flush = [&](const StPhase& ph) {
     if (ph.log2c < kStMinLog2C) return;
     const uint32_t c = 1u << ph.log2c;
     for (int p = threadIdx.x; p < kStPool; p += blockDim.x) {
@@ -1617,18 +1623,28 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   };
   // level l's grads = elements 2 (l & 1) .. of level pair l / 2 (tile_level:
   // chunk lp / 2 of lane half lp % 2); a coarse twin adds its coarse grads
-  auto unit_grads = [&](Unit& q, int l) {
-    if (!q.act) return;
+  // a level's grads as two loads (fine, coarse twin) issued ahead of their
+  // use (grads_take): the staged loop loads level l + 1's while level l runs
+  struct GradLd {
+    float2 f, t;
+  };
+  auto grads_issue = [&](const Unit& q, int l) {
+    GradLd gl{make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+    if (!q.act) return gl;
     const int lp = l >> 1, o = 4 * (64 * (lp >> 1) + 32 * (lp & 1)) + 2 * (l & 1);
-    float2 gq = *reinterpret_cast<const float2*>(q.tb + o);
-    if (q.tw) {
-      const float2 t2 = *reinterpret_cast<const float2*>(q.tw + o);
-      gq = make_float2(gq.x + t2.x, gq.y + t2.y);
-    }
+    gl.f = *reinterpret_cast<const float2*>(q.tb + o);
+    if (q.tw) gl.t = *reinterpret_cast<const float2*>(q.tw + o);
+    return gl;
+  };
+  auto grads_take = [&](Unit& q, const GradLd& gl) {
+    if (!q.act) return;
+    // fine + coarse twin (the fused ring's order); no twin: the fine grads as they are
+    const float2 gq = q.tw ? make_float2(gl.f.x + gl.t.x, gl.f.y + gl.t.y) : gl.f;
     q.g0 = gq.x;
     q.g1 = gq.y;
     bad |= !(fabsf(gq.x + gq.y) <= 3.402823466e38f);
   };
+  auto unit_grads = [&](Unit& q, int l) { grads_take(q, grads_issue(q, l)); };
   auto unit_at = [&](int64_t it, int l) {
     Unit q = unit_base(it);
     unit_grads(q, l);
@@ -1641,9 +1657,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   //   kDirect: direct store,
   //   kMerged: the merge table (int64 at the level's block scale `mscale`)
   enum { kStaged = 0, kDirect = 1, kMerged = 2 };
-  auto level = [&](const Unit& q, const int l, const int mode, const float mscale) {
+  auto level = [&](const Unit& q, const int l, const int mode, const float mscale, const StPhase& ph) {
     if (!q.act) return;
-    const StPhase ph = st_phase(l, log2T, sh);
     const bool staged = mode == kStaged && ph.log2c >= kStMinLog2C;
     int32_t cell[3];
     float w[3];
@@ -1769,7 +1784,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
         __hip_atomic_fetch_max(mh_bound + l, __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  if (n_merge < 16) st_init(n_merge, par);
+  // staging phases of 2^lpp levels where each level owns whole bins
+  const int lpp = log2T >= sh ? HN_SC_LPP : 0;
+  auto phase_of = [&](int l) { return st_phase(l, log2T, sh, l + (1 << lpp) <= 16 ? lpp : 0); };
+  if (n_merge < 16) st_init(phase_of(n_merge), par);
   __syncthreads();
   for (int l = 0; l < n_merge; ++l) {
     {
@@ -1779,7 +1797,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const int S0 = 40 - eb;
       const int S = S0 > 127 ? 127 : (S0 < -126 ? -126 : S0);
       const float mscale = ldexpf(1.f, S);
-      for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kMerged, mscale);
+      for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kMerged, mscale, st_phase(l, log2T, sh));
       __syncthreads();   // the level's sums are complete
       const bool failed = mh_fail != 0u;   // uniform
       if (!failed) {
@@ -1811,7 +1829,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
         __syncthreads();   // every lane has read mh_fail
         mh_clear();
         if (threadIdx.x == 0) mh_fail = 0u;
-        for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kDirect, 1.f);
+        for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kDirect, 1.f, st_phase(l, log2T, sh));
       }
       __syncthreads();   // the table is empty again
     }
@@ -1820,14 +1838,26 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // their records through the staging pool, one phase per (unit round, level)
   for (int64_t it = 0; it < n_it && n_merge < 16; ++it) {
     Unit q = unit_base(it);
-    for (int l = n_merge; l < 16; ++l) {
-      unit_grads(q, l);
-      level(q, l, kStaged, 1.f);
+#if HN_SC_PF
+    GradLd gl = grads_issue(q, n_merge);
+#endif
+    for (int l = n_merge; l < 16;) {
+      const StPhase ph = phase_of(l);
+      const int np = l + (1 << lpp) <= 16 ? 1 << lpp : 1;
+      for (int j = 0; j < np; ++j, ++l) {
+#if HN_SC_PF
+        grads_take(q, gl);
+        if (l + 1 < 16) gl = grads_issue(q, l + 1);   // in flight across this level's work
+#else
+        unit_grads(q, l);
+#endif
+        level(q, l, kStaged, 1.f, ph);
+      }
       __syncthreads();   // the phase's records are in the pool, its counts final
-      st_flush(l);
+      st_flush(ph);
       // the next phase's bins (other parity), counts unchanged by the flush
-      const int ln = l + 1 < 16 ? l + 1 : (it + 1 < n_it ? n_merge : 16);
-      if (ln < 16) st_init(ln, par ^ 1);
+      const int ln = l < 16 ? l : (it + 1 < n_it ? n_merge : 16);
+      if (ln < 16) st_init(phase_of(ln), par ^ 1);
       __syncthreads();   // the pool is free again
       par ^= 1;
     }
