@@ -559,6 +559,61 @@ HN_DEV void wgrad_n(const char* Xb, const int (&ablk)[NA], const int (&bblk)[NB]
   }
 }
 
+template <int I, int N, typename F>
+HN_DEV void static_for(F&& f) {
+  if constexpr (N > 0) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N - 1>(f);
+  }
+}
+
+// A weight-gradient block's operands read into registers ahead of its
+// products (WgOps), and the products then issued in the gaps of a later
+// data-path GEMM (WgX, gemm_w / gemm_w2's `xt`): the image reads leave before
+// that GEMM's own image writes (a wave's LDS accesses execute in order), and
+// the products -- the same ones, per accumulator in the same order as
+// wgrad_n's -- keep the matrix pipe busy while the chain waits on its own
+// results and splits.  NoX: no extra products.
+template <int NA, int NB>
+struct WgOps {
+  SP<2> a[2][NA], b[2][NB];   // [K = 16 chunk cc][operand]
+};
+template <int NA, int NB>
+HN_DEV void wg_load(WgOps<NA, NB>& o, const char* Xb, const int (&ablk)[NA], const int (&bblk)[NB], int lane) {
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) {
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) o.a[cc][j].p[q] = img_operand(Xb, ablk[j], q, cc, lane);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) o.b[cc][j].p[q] = img_operand(Xb, bblk[j], q, cc, lane);
+  }
+}
+struct NoX {
+  static constexpr int per(int) { return 0; }
+  template <int C>
+  HN_DEV void run() const {}
+};
+// the 2 * NA * NB products of a WgOps (cc-major, as wgrad_n) spread over NC chunks
+template <int NA, int NB, int NC>
+struct WgX {
+  const WgOps<NA, NB>& o;
+  f32x16* acc;
+  static constexpr int P = 2 * NA * NB;
+  static constexpr int lo(int c) { return c * P / NC; }
+  static constexpr int per(int c) { return 3 * (lo(c + 1) - lo(c)); }   // MFMAs at chunk c
+  template <int C>
+  HN_DEV void run() const {
+    static_for<lo(C), lo(C + 1) - lo(C)>([&](auto pc) {
+      constexpr int p = decltype(pc)::value, cc = p / (NA * NB), ja = p % (NA * NB) / NB, jb = p % NB;
+      acc[NB * ja + jb] = mfma_split<2>(o.a[cc][ja], o.b[cc][jb], acc[NB * ja + jb]);
+    });
+  }
+};
+
 // ---- weight-fragment stream ----------------------------------------------
 // A tile's 15 data-path GEMMs read their packed A-fragment groups (one 1-KiB
 // dwordx4 load per wave: 4 f32 k-steps, or one bf16 part of 8 k-steps) in a
@@ -629,13 +684,6 @@ struct WRing {
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
   return frag_load(P, off, lane);
 }
-template <int I, int N, typename F>
-HN_DEV void static_for(F&& f) {
-  if constexpr (N > 0) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N - 1>(f);
-  }
-}
 
 // (offsets are constexpr-evaluated: left to the optimiser, the region
 // arithmetic of group_off stays as scalar loops in the kernel)
@@ -674,8 +722,14 @@ HN_DEV void swp_pattern() {
 // acc += A(segment SEG of the stream) . B, bval(s) = B operand of f32 k-step s.
 // IMG >= 0: chunk c's first two B parts also go to image tile IMG + c / 2 at
 // quad offset F4B + 4 (c % 2) (put_parts; Xb = the wave's images).
-template <int SEG, int IMG = -1, int F4B = 0, typename BF>
-HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, char* Xb = nullptr) {
+// XT: extra independent MFMAs issued after chunk c's own (WgX; NoX: none),
+// their VALU slots sharing the next chunk's split (kSplitV VALU per split).
+template <int NS, bool PAIR>
+constexpr int kSplitV = NS == 3 ? 36 : (PAIR ? 24 : 21);
+constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
+template <int SEG, int IMG = -1, int F4B = 0, typename BF, typename XT = NoX>
+HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, char* Xb = nullptr,
+                     const XT& xt = XT{}) {
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
   if constexpr (NS > 0 && KS > 8) {   // split-f32, next chunk's split in the MFMA gaps
@@ -691,9 +745,11 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
       });
       if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
       acc = mfma_split<NS>(a, b, acc);
+      xt.template run<c>();
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 6 : 3, NS == 3 ? 6 : 7>();
+        constexpr int M = NS + XT::per(c);
+        swp_pattern<M, XT::per(c) ? ceil_div(kSplitV<NS, false>, M) : (NS == 3 ? 6 : 7)>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -708,6 +764,7 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
       if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
       acc = mfma_split<NS>(a, b, acc);
+      xt.template run<c>();
       __builtin_amdgcn_sched_barrier(0);
     });
   } else {
@@ -716,6 +773,7 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
       const f32x4 a = wring_take<START + g>(w, P, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma(a[j], bval(4 * g + j), acc);
+      xt.template run<g>();
       __builtin_amdgcn_sched_barrier(0);
     });
   }
@@ -724,8 +782,9 @@ HN_DEV f32x16 gemm_w(WRing& w, const float* P, f32x16 acc, int lane, BF bval, ch
 
 // acc0 / acc1 += blocks 0 / 1 of the paired segment SEG . B: one B split per
 // chunk for both blocks, and two independent accumulator chains
-template <int SEG, int IMG = -1, int F4B = 0, typename BF>
-HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int lane, BF bval, char* Xb = nullptr) {
+template <int SEG, int IMG = -1, int F4B = 0, typename BF, typename XT = NoX>
+HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int lane, BF bval, char* Xb = nullptr,
+                    const XT& xt = XT{}) {
   constexpr int R = kSegs[SEG].r, KS = kRegKS[R], NS = seg_ns(kSegs[SEG]), START = seg_start(SEG);
   static_assert(kSegs[SEG].ob < 0, "paired segment");
   static_assert(IMG < 0 || NS >= 2, "image sinks take split B operands");
@@ -746,9 +805,11 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
       });
       if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
+      xt.template run<c>();
       if constexpr (c + 1 < NC) {
         b = splitn<NS>([&](int j) { return bval(8 * (c + 1) + j); });
-        swp_pattern<NS == 3 ? 12 : 6, NS == 3 ? 3 : 4>();
+        constexpr int M = 2 * NS + XT::per(c);
+        swp_pattern<M, XT::per(c) ? ceil_div(kSplitV<NS, true>, M) : (NS == 3 ? 3 : 4)>();
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -768,6 +829,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
       if constexpr (IMG >= 0) put_parts<NS>(Xb, IMG + c / 2, F4B + 4 * (c % 2), b, lane);
       mfma_split2<NS>(a0, a1, b, acc0, acc1);
+      xt.template run<c>();
       __builtin_amdgcn_sched_barrier(0);
     });
   } else {
@@ -780,6 +842,7 @@ HN_DEV void gemm_w2(WRing& w, const float* P, f32x16& acc0, f32x16& acc1, int la
         acc0 = mfma(a0[j], bval(4 * g + j), acc0);
         acc1 = mfma(a1[j], bval(4 * g + j), acc1);
       }
+      xt.template run<g>();
       __builtin_amdgcn_sched_barrier(0);
     });
   }
@@ -791,12 +854,14 @@ constexpr int seg_of(int r) {   // first stream segment of region r
   return -1;
 }
 // acc[0..1] += both output blocks of region R . B (image sink: gemm_w)
-template <int R, int IMG = -1, int F4B = 0, typename BF>
-HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, char* Xb = nullptr) {
+template <int R, int IMG = -1, int F4B = 0, typename BF, typename XT = NoX>
+HN_DEV void gemm2(WRing& w, const float* P, f32x16 acc[2], int lane, BF bval, char* Xb = nullptr,
+                  const XT& xt = XT{}) {
   constexpr int S = seg_of(R);
   if constexpr (kSegs[S].ob < 0) {
-    gemm_w2<S, IMG, F4B>(w, P, acc[0], acc[1], lane, bval, Xb);
+    gemm_w2<S, IMG, F4B>(w, P, acc[0], acc[1], lane, bval, Xb, xt);
   } else {
+    static_assert(std::is_same<XT, NoX>::value, "extra products go to paired segments");
     acc[0] = gemm_w<S, IMG, F4B>(w, P, acc[0], lane, bval, Xb);
     acc[1] = gemm_w<S + 1>(w, P, acc[1], lane, bval);
   }
@@ -857,6 +922,9 @@ HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
     }
 }
 
+#ifndef HN_B1_WGX   // 1: weight-gradient products inside the next data-path GEMM (WgX)
+#define HN_B1_WGX 1
+#endif
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
@@ -896,6 +964,58 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     }
   }
   tile_lds_order();
+#if HN_B1_WGX
+  // Each layer's weight-gradient products run inside the NEXT data-path GEMM
+  // (WgX): its operands are read here, before that GEMM's image writes, and
+  // its MFMAs fill the chain's gaps -- per accumulator the same products in
+  // the same order as the wgrad_n form below (bitwise-equal dW).
+  // ---- color_net.2 (dW rows >= 3 are discarded) inside color_net.2^T ----
+  WgOps<1, 2> w_c2;
+  {
+    const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
+    wg_load(w_c2, Xb, ab, bb, lane);
+  }
+  const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
+  f32x16 dc1[2] = {zero16(), zero16()};
+  gemm2<R_B4>(wr, P, dc1, lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; }, nullptr, WgX<1, 2, 1>{w_c2, dw.c2});
+  mask_bits(dc1[0], mc1, 0);
+  mask_bits(dc1[1], mc1, 1);
+  // ---- color_net.1 (dc1 image over c1) ----
+  f32x16 dc0[2] = {zero16(), zero16()};
+  gemm2<R_B3, kBC1>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; }, Xb);
+  mask_bits(dc0[0], mc0, 0);
+  mask_bits(dc0[1], mc0, 1);
+  tile_lds_order();
+  // ---- color_net.0 (dc0 image over c0; B = [sh16 | sigma | geo15]), color_net.1's dW inside ----
+  WgOps<2, 2> w_c1;
+  {
+    const int ab[2] = {kBC1, kBC1 + 1}, bb[2] = {kBC0, kBC0 + 1};
+    wg_load(w_c1, Xb, ab, bb, lane);            // dw.c1[2 * nb + kb]
+  }
+  f32x16 ds1 = gemm_w<seg_of(R_B2G), kBC0>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; }, Xb,
+                                           WgX<2, 2, 4>{w_c1, dw.c1});
+  if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
+  tile_lds_order();
+  // ---- sigma_net.1 (ds1 image over dc1's first tile; rows 16..31 discarded), color_net.0's dW inside ----
+  WgOps<2, 1> w_c0;
+  {
+    const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBC0in};
+    wg_load(w_c0, Xb, ab, bb, lane);
+  }
+  f32x16 dh0[2] = {zero16(), zero16()};
+  gemm2<R_B1, kBC1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; }, Xb, WgX<2, 1, 1>{w_c0, dw.c0});
+  mask_bits(dh0[0], mh0, 0);
+  mask_bits(dh0[1], mh0, 1);
+  tile_lds_order();
+  // ---- sigma_net.0 (dh0 image over dc0), sigma_net.1's dW inside ----
+  WgOps<1, 2> w_s1;
+  {
+    const int ab[1] = {kBC1}, bb[2] = {kBH0, kBH0 + 1};
+    wg_load(w_s1, Xb, ab, bb, lane);
+  }
+  const f32x16 dfeat = gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; },
+                                                  Xb, WgX<1, 2, 4>{w_s1, dw.s1});
+#else
   // ---- color_net.2 (dW rows >= 3 are discarded) ----
   {
     const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
@@ -937,6 +1057,7 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   // ---- sigma_net.0 (dh0 image over dc0) ----
   const f32x16 dfeat =
       gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; }, Xb);
+#endif
   tile_lds_order();
   {
     const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBF};
@@ -1505,10 +1626,10 @@ HN_DEV StPhase st_phase(int l, int log2T, int shift, int lg2n = 0) {
   return ph;
 }
 #ifndef HN_SC_PF   // the next level's grads loaded while a level runs
-#define HN_SC_PF 1
+#define HN_SC_PF 0
 #endif
 #ifndef HN_SC_LPP   // log2 levels per staging phase (one block barrier pair per phase)
-#define HN_SC_LPP 0
+#define HN_SC_LPP 1
 #endif
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
