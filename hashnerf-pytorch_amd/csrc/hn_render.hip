@@ -1905,8 +1905,11 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
         __hip_atomic_fetch_max(mh_bound + l, __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  // staging phases of 2^lpp levels where each level owns whole bins
-  const int lpp = log2T >= sh ? HN_SC_LPP : 0;
+  // staging phases of 2^lpp levels where each level owns whole bins and the
+  // pool still holds >= 2^kStMinLog2C records per bin (T=19: 2 levels per
+  // phase, 32 records per bin; T=22: 1 level, 8 per bin)
+  const int lg_bins = log2T - sh;   // log2 bins per level
+  const int lpp = lg_bins < 0 ? 0 : max(0, min(HN_SC_LPP, kStLog2 - kStMinLog2C - lg_bins));
   auto phase_of = [&](int l) { return st_phase(l, log2T, sh, l + (1 << lpp) <= 16 ? lpp : 0); };
   if (n_merge < 16) st_init(phase_of(n_merge), par);
   __syncthreads();
