@@ -302,6 +302,8 @@ def main():
     ap.add_argument("--dp-chunks", type=int, default=1,
                     help="N > 1: segments of the sharded table exchange, each reduce-scattered as soon as "
                          "the owner pass has formed it (1: one exchange after the backward)")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="A/B: draw each step's batch at its start (no side-stream prefetch)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -360,6 +362,9 @@ def main():
     tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0, ray_order=args.ray_order)
     tr.skip_dead_rows = not args.dense_table_step
     tr.dp_chunks = args.dp_chunks
+    # the next step's rays and uniforms drawn on a side stream beside the
+    # backward (the same draws; Trainer.prefetch)
+    tr.prefetch = not args.no_prefetch
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1

@@ -564,6 +564,17 @@ class Trainer:
         self.dp_chunks = 1
         self._xchg = None
         self._owner_st = None
+        # self-driving loops (bench.py): the next step's batch -- device ray
+        # sampler and the jitter / importance uniforms -- is drawn on a side
+        # stream as soon as this step's forward is enqueued, so it runs beside
+        # the backward instead of ahead of the next forward.  The draws and
+        # their order are those of draw_batch at the start of the next step
+        # (bitwise the same trajectory).  Opt-in: a caller that draws its own
+        # batches (draw_batch + step(i, batch)) must leave it off, or the
+        # prefetch consumes the next step's random numbers first.
+        self.prefetch = False
+        self._pf = None          # (step, batch, ready event) drawn ahead
+        self._side = None
 
     def _train_image(self):
         """np.random.choice(i_train) (run_nerf.py:578) from the host generator."""
@@ -730,10 +741,41 @@ class Trainer:
                                self.embed_fn.finest_resolution, self.cpu_gen)
         return dict(rays=rays, target=target, t_rand=t_rand, u=u, tv=tv)
 
+    def _prefetch(self, i: int):
+        """draw_batch(i) on the side stream, after the work enqueued so far on
+        the current stream (the sampler's workspace is shared)."""
+        cur = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._side.wait_event(ev)
+        with torch.cuda.stream(self._side):
+            b = self.draw_batch(i)
+            done = torch.cuda.Event()
+            done.record(self._side)
+        self._pf = (i, b, done)
+
+    def _take_prefetched(self, i: int):
+        """The batch drawn ahead for step i (None if there is none): the
+        current stream waits for it and takes its tensors over."""
+        pf, self._pf = self._pf, None
+        if pf is None or pf[0] != i:
+            return None
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(pf[2])
+        for k in ("rays", "target", "t_rand", "u"):
+            if torch.is_tensor(pf[1][k]):
+                pf[1][k].record_stream(cur)
+        return pf[1]
+
     def _fused_forward_backward(self, i: int, batch=None):
         a = self.args
         if self._grads is None:
             self._fused_setup()
+        pf = self.prefetch and batch is None and self.device.type == "cuda"
+        if pf:
+            batch = self._take_prefetched(i)
         if batch is None:
             batch = self.draw_batch(i)
         rays, target, t_rand, u = batch["rays"], batch["target"], batch["t_rand"], batch["u"]
@@ -741,6 +783,8 @@ class Trainer:
         if rays.shape[0] == 0:
             return self._empty_rank_grads(batch)
         out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
+        if pf:
+            self._prefetch(i + 1)
         tv = mv = cubes = None
         if batch["tv"] is not None:
             cubes, mv0 = batch["tv"]

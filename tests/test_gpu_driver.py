@@ -232,3 +232,29 @@ def test_device_fault_word_clear_after_fused_steps(hn):
     assert hn._lib.lib().hn_device_faults(C.byref(w), 0) == 0
     assert w.value == 0
     hn._lib.check_device_faults()
+
+
+@pytest.mark.parametrize("batching", [True, False], ids=["per_image", "pool"])
+def test_trainer_prefetch_same_trajectory(hn, batching):
+    """Trainer.prefetch: the next step's batch (device sampler, jitter and
+    importance uniforms, TV cubes; or the use_batching pool) drawn on a side
+    stream beside the backward gives bitwise the trajectory of drawing it at
+    the step's start -- the same draws in the same order -- over 7 steps
+    across the precrop boundary (precrop_iters 4) with TV through step 5."""
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(48, 48, 3, DEV, seed=0)
+    res = {}
+    for pf in (False, True):
+        args = default_args(N_rand=256, log2_hashmap_size=13, tv_loss_weight=1e-4, tv_until=5,
+                            precrop_iters=4, sparse_loss_weight=1e-3, no_batching=batching)
+        tr = Trainer(args, data, DEV, seed=5)
+        tr.prefetch = pf
+        torch.manual_seed(17)
+        losses = [float(tr.step()[0]) for _ in range(7)]
+        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+        res[pf] = (losses, tr.embed_fn.table.detach().clone(), [p.detach().clone() for p in ws])
+    a, b = res[False], res[True]
+    assert a[0] == b[0]
+    assert torch.equal(a[1], b[1])
+    for x, y in zip(a[2], b[2]):
+        assert torch.equal(x, y)
