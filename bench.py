@@ -302,8 +302,8 @@ def main():
     ap.add_argument("--dp-chunks", type=int, default=1,
                     help="N > 1: segments of the sharded table exchange, each reduce-scattered as soon as "
                          "the owner pass has formed it (1: one exchange after the backward)")
-    ap.add_argument("--no-prefetch", action="store_true",
-                    help="A/B: draw each step's batch at its start (no side-stream prefetch)")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="A/B: draw the next step's batch on a side stream beside the backward")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -362,9 +362,11 @@ def main():
     tr = Trainer(targs, data, dev, rank=rank, world=world, seed=0, ray_order=args.ray_order)
     tr.skip_dead_rows = not args.dense_table_step
     tr.dp_chunks = args.dp_chunks
-    # the next step's rays and uniforms drawn on a side stream beside the
-    # backward (the same draws; Trainer.prefetch)
-    tr.prefetch = not args.no_prefetch
+    # --prefetch: the next step's rays and uniforms drawn on a side stream
+    # beside the backward (the same draws; Trainer.prefetch).  Off by default:
+    # measured slower (r05k: 0.996 vs 0.982 ms per step) -- the cross-stream
+    # waits cost more than the ~20 us of sampler and RNG launches they move
+    tr.prefetch = args.prefetch
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1

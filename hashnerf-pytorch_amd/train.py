@@ -571,7 +571,10 @@ class Trainer:
         # their order are those of draw_batch at the start of the next step
         # (bitwise the same trajectory).  Opt-in: a caller that draws its own
         # batches (draw_batch + step(i, batch)) must leave it off, or the
-        # prefetch consumes the next step's random numbers first.
+        # prefetch consumes the next step's random numbers first.  Measured
+        # slower at config 2 (r05k: 0.996 vs 0.982 ms per step: the
+        # cross-stream waits cost more than the launches they move), so off
+        # unless asked for (bench.py --prefetch).
         self.prefetch = False
         self._pf = None          # (step, batch, ready event) drawn ahead
         self._side = None
