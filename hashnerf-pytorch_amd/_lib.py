@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 12                # HN_ABI_VERSION
+ABI_VERSION = 13                # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 9728      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -48,13 +48,18 @@ class HnRenderCfg(C.Structure):
 _P = C.c_void_p
 
 
+class HnRenderLoss(C.Structure):
+    _fields_ = [("target", _P), ("tv", _P), ("n_tv", C.c_int32), ("world", C.c_float), ("sparse_w", C.c_float),
+                ("tv_w", C.c_float), ("out", _P), ("counter", _P)]
+
+
 class HnRenderFwdArgs(C.Structure):
     _fields_ = [("n_rays", C.c_int64), ("rays", _P), ("t_vals", _P), ("t_rand", _P), ("u", _P),
                 ("noise_c", _P), ("noise_f", _P), ("table", _P), ("coarse", HnMlp), ("fine", HnMlp),
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
                 ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
-                ("fine_src", _P), ("feat", _P)]
+                ("fine_src", _P), ("feat", _P), ("loss", C.POINTER(HnRenderLoss))]
 
 
 class HnRadamTensor(C.Structure):
@@ -73,7 +78,8 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
                 ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
-                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32)]
+                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32),
+                ("draw_ready", C.c_int32)]
 
 
 class HnTvArgs(C.Structure):

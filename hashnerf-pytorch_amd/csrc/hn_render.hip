@@ -61,6 +61,18 @@ struct RenderK {
   float *z_coarse, *z_fine, *raw_c, *raw_f;
   uint8_t* fine_src;
   float* feat;    // [B][8 tiles][1024] saved features or NULL
+  // ABI 13 fused training loss (hn_render_loss; target NULL = none): the
+  // composite backward of both passes into draw, the loss value reduced by
+  // the last workgroup from per-workgroup fp64 partials
+  const float* target;
+  float lgm, lsparse;   // (g / world) / (3 B) and g * sparse_w with g = 1: hn_loss_bwd's op forms
+  float* draw;          // [B][64 + 192][4] (the backward's pre-pass output, in the workspace)
+  double* lpart;        // [workgroups][4] (in the workspace's dW-slab region, free until the backward)
+  uint32_t* lcount;
+  const float* ltv;
+  int32_t n_tv;
+  float world, sparse_w, tv_w;
+  float* lout;
 };
 
 
@@ -88,6 +100,7 @@ struct B1K {
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   float* dfeat_f;       // split backward: [B][6 fine tiles][1024] fine-pass feature grads (tile order)
+  int32_t zero_book;    // ABI 13 draw_ready: the MLP-backward kernel resets the overflow book
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -253,6 +266,63 @@ __device__ unsigned long long g_fwd_prof[8];
 // 0.301-0.313 ms; profiles/r04/r04e, r04f.)
 constexpr int kFwdBlockWaves = kFwdWaves;
 
+// Fused loss value: the workgroup's fp64 partials (squared errors fine and
+// coarse, entropy sums; wave order fixed), then the last workgroup to finish
+// (ticket from an agent-scope counter, released / acquired as
+// MI355X_MICROARCH.md's hand-off recipe prescribes) sums every workgroup's
+// partials in a fixed order and writes hn_loss_fwd's out[4]; it resets the
+// counter for the next launch.  Every wave of the workgroup calls this.
+HN_DEV void loss_partials(const RenderK& k, double se, double se0, double ent, int wave, int lane) {
+  __shared__ double lp[kFwdBlockWaves][3];
+  __shared__ uint32_t last;
+  if (lane == 0) {
+    lp[wave][0] = se;
+    lp[wave][1] = se0;
+    lp[wave][2] = ent;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[3] = {0.0, 0.0, 0.0};
+    for (int w = 0; w < kFwdBlockWaves; ++w)
+      for (int q = 0; q < 3; ++q) t[q] += lp[w][q];
+    for (int q = 0; q < 3; ++q) k.lpart[4 * (size_t)blockIdx.x + q] = t[q];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t tk = __hip_atomic_fetch_add(k.lcount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == gridDim.x - 1 ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  double a[3] = {0.0, 0.0, 0.0};
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+    for (int q = 0; q < 3; ++q) a[q] += k.lpart[4 * (size_t)b + q];
+  for (int q = 0; q < 3; ++q) a[q] = wave_sum(a[q]);
+  __syncthreads();   // lp is read again below
+  if (lane == 0)
+    for (int q = 0; q < 3; ++q) lp[wave][q] = a[q];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int w = 0; w < kFwdBlockWaves; ++w)
+      for (int q = 0; q < 3; ++q) t[q] += lp[w][q];
+    for (int j = 0; j < k.n_tv; ++j) t[3] += (double)k.ltv[j];
+    // hn_loss_fwd's value (loss_fwd_block)
+    const double N = 3.0 * (double)k.B;
+    const float mse = (float)(t[0] / N), mse0 = (float)(t[1] / N);
+    const float ent = (float)t[2];
+    k.lout[0] = (mse + mse0) / k.world + k.sparse_w * ent + (k.ltv ? k.tv_w * (float)t[3] : 0.f);
+    k.lout[1] = mse;
+    k.lout[2] = mse0;
+    k.lout[3] = ent;
+    *k.lcount = 0u;
+  }
+}
+
 __global__ __launch_bounds__(64 * kFwdBlockWaves)
 __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
 void render_fwd_kernel(RenderK k) {
@@ -346,6 +416,29 @@ void render_fwd_kernel(RenderK k) {
     k.acc0[ray] = co.acc;
     k.sparsity0[ray] = co.entropy;
   }
+  double l_se0 = 0.0;   // fused loss: this ray's squared errors (coarse, fine)
+  if (k.target) {
+    // d loss / d rgb0, d loss / d entropy0 (hn_loss_bwd_elem's op forms), then
+    // the coarse raw2outputs backward in place over rawb (free until the
+    // merge sort below uses it as scratch): render_comp_bwd_kernel's values
+    CompGrad g;
+    g.has_rgb = g.has_entropy = true;
+    g.has_acc = g.has_depth = false;
+    g.acc = g.depth = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float e = co.rgb[c] - k.target[3 * ray + c];
+      g.rgb[c] = k.lgm * (2.f * e);
+      l_se0 += (double)(e * e);
+    }
+    g.entropy = k.lsparse;
+    composite_bwd<1>(rawb, zc, k.noise_c ? k.noise_c + ray * kSc : nullptr, kSc, r.dnorm, k.white != 0, g,
+                     nullptr, nullptr, rawb, lane);
+    lds_fence_wave();
+    *reinterpret_cast<float4*>(k.draw + ((size_t)ray * (kSc + kSf) + lane) * 4) =
+        *reinterpret_cast<const float4*>(rawb + 4 * lane);
+    lds_fence_wave();
+  }
 
   // ---- importance sampling (:547-551) ----
   if (lane < kSc - 1) bins[lane] = .5f * (zc[lane + 1] + zc[lane]);
@@ -422,6 +515,27 @@ void render_fwd_kernel(RenderK k) {
     k.depth[ray] = fo.depth;
     k.acc[ray] = fo.acc;
     k.sparsity[ray] = fo.entropy;
+  }
+  if (k.target) {
+    CompGrad g;
+    g.has_rgb = g.has_entropy = true;
+    g.has_acc = g.has_depth = false;
+    g.acc = g.depth = 0.f;
+    double l_se = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float e = fo.rgb[c] - k.target[3 * ray + c];
+      g.rgb[c] = k.lgm * (2.f * e);
+      l_se += (double)(e * e);
+    }
+    g.entropy = k.lsparse;
+    lds_fence_wave();   // the composite's reads of rawb are done (in-order LDS; compiler order)
+    composite_bwd<3>(rawb, zs, k.noise_f ? k.noise_f + ray * kSf : nullptr, kSf, r.dnorm, k.white != 0, g,
+                     nullptr, nullptr, rawb, lane);
+    lds_fence_wave();
+    float4* dst = reinterpret_cast<float4*>(k.draw + ((size_t)ray * (kSc + kSf) + kSc) * 4);
+    for (int j = lane; j < kSf; j += 64) dst[j] = *reinterpret_cast<const float4*>(rawb + 4 * j);
+    loss_partials(k, l_se, l_se0, (double)fo.entropy + (double)co.entropy, wave, lane);
   }
 #if HN_PROFILE
   HN_FT(5);
@@ -2344,6 +2458,16 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
   }
 }
 
+// The binned scatter's overflow book starts empty (count, per bin, cursors,
+// the scatter blocks' slab-block counter): reset by workgroup 0 of the first
+// kernel of the backward.
+HN_DEV void zero_ovf_book(const B1K& k) {
+  const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
+  uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
+  for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
+  if (threadIdx.x == 0) o[1 + 3 * k.nbins] = 0u;   // the scatter kernel's slab-block counter (ob.slab_next)
+}
+
 // Composite backward pre-pass (raw2outputs backward, run_nerf_helpers.py:577-628
 // via the :541 / :558 chain): one wave per (ray, pass) at full occupancy
 // writes d raw of every sample, so the MLP units only load one float4 per
@@ -2352,12 +2476,7 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   __shared__ float lds[kFwdWaves][kSf * 5];
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (k.bins && blockIdx.x == 0) {   // binned scatter: no overflow records yet (count, per bin, cursors)
-    const size_t nrec = bin_records(k.nbins, k.bin_cap, k.B);
-    uint32_t* o = ovf_book(reinterpret_cast<uint32_t*>(k.bins + 4 * nrec), nrec, k.nbins).cnt;
-    for (int i = threadIdx.x; i < 1 + 2 * k.nbins; i += blockDim.x) o[i] = 0u;
-    if (threadIdx.x == 0) o[1 + 3 * k.nbins] = 0u;   // the scatter kernel's slab-block counter (ob.slab_next)
-  }
+  if (k.bins && blockIdx.x == 0) zero_ovf_book(k);   // binned scatter: no overflow records yet
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
   const int64_t ray = w >> 1;
@@ -2489,6 +2608,7 @@ void render_bwd_kernel(B1K k) {
   int* sync = reinterpret_cast<int*>(gsl + kGsLds);
   stage_grid_sizes(k.g, gsl);
   if (threadIdx.x < kSyncInts) sync[threadIdx.x] = 0;
+  if (k.zero_book && blockIdx.x == 0) zero_ovf_book(k);   // no composite pre-pass ran (draw_ready)
   __syncthreads();
   const Ring ring{slots, &sync[2], &sync[5], &sync[5 + kSlots], gsl};
   const int64_t nb = gridDim.x;
@@ -3060,7 +3180,33 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.rgb0 = a->rgb0; k.depth0 = a->depth0; k.acc0 = a->acc0; k.sparsity0 = a->sparsity0;
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
+  k.target = nullptr;
+  k.draw = nullptr; k.lpart = nullptr; k.lcount = nullptr; k.ltv = nullptr; k.lout = nullptr;
+  k.n_tv = 0;
+  k.lgm = k.lsparse = k.world = k.sparse_w = k.tv_w = 0.f;
+  if (a->loss) {   // ABI 13: the training loss fused in (hn_render_loss)
+    const hn_render_loss& L = *a->loss;
+    if (!L.target || !L.out || !L.counter || !a->feat || (L.n_tv && !L.tv)) return HN_E_NULL;
+    if (a->n_rays % kFwdBlockWaves || L.n_tv < 0 || L.n_tv > 64 || !(L.world > 0.f)) return HN_E_SHAPE;
+    k.target = L.target;
+    // hn_loss_bwd's upstream factors with g_loss = 1: (g / world) / (3 n), g * sparse_w
+    const float g = 1.f;
+    k.lgm = (g / L.world) / (float)(3 * a->n_rays);
+    k.lsparse = g * L.sparse_w;
+    // the backward's d raw region and, for the partials, the dW slabs (written by the backward later)
+    float* slab = Pf + G_END;
+    k.lpart = reinterpret_cast<double*>(slab);
+    k.draw = slab + (size_t)kBwdBlocks * kSlabSlots * W_END + (size_t)a->n_rays * kDcRay;
+    k.lcount = L.counter;
+    k.ltv = L.n_tv ? L.tv : nullptr;
+    k.n_tv = L.n_tv;
+    k.world = L.world; k.sparse_w = L.sparse_w; k.tv_w = L.tv_w;
+    k.lout = L.out;
+  }
   const unsigned blocks = (unsigned)((a->n_rays + kFwdBlockWaves - 1) / kFwdBlockWaves);
+  static_assert((size_t)kBwdBlocks * kSlabSlots * W_END * 4 >= (size_t)(1 << 20) * 32,
+                "the loss partials of up to 2^20 workgroups fit the dW-slab region");
+  if (a->loss && blocks > (1u << 20)) return HN_E_SHAPE;
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdBlockWaves), 0, s, k);
 #if HN_PROFILE
   {
@@ -3139,6 +3285,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     return HN_E_NULL;
   if ((!a->d_table && !a->table_step) || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
   if (a->d_table_mode < 0 || a->d_table_mode > 3) return HN_E_SHAPE;
+  if (a->draw_ready && !a->weights_packed) return HN_E_SHAPE;   // d raw lives in the forward's workspace
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -3212,8 +3359,12 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     const size_t tb = ((size_t)16 << T) * 2 * sizeof(float);
     if ((st = hip_status(hipMemsetAsync(a->d_table, 0, tb, s)))) return st;
   }
-  hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
-                     dim3(64 * kFwdWaves), 0, s, k);
+  k.zero_book = 0;
+  if (!a->draw_ready)
+    hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
+                       dim3(64 * kFwdWaves), 0, s, k);
+  else
+    k.zero_book = k.bins != nullptr;   // the pre-pass's other duty moves to the MLP-backward kernel
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
   if (mode == kModeSplit)

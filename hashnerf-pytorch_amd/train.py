@@ -577,6 +577,10 @@ class Trainer:
         # unless asked for (bench.py --prefetch).
         self.prefetch = False
         self._pf = None          # (step, batch, ready event) drawn ahead
+        # explicit mode: the loss, its gradients and the composite backward
+        # fused into the render forward (ABI 13; batches of a multiple of 4
+        # rays) instead of hn_loss_fwd_bwd + the backward's composite pre-pass
+        self.fuse_loss = True
         self._side = None
 
     def _train_image(self):
@@ -718,6 +722,7 @@ class Trainer:
         self._binned = HF.L.lib().hn_render_scatter_mode(self._cfg, a.N_rand) == 2
         self._gws = HF.zeros_like_all(self._ws)
         self._one = torch.ones((), device=self.device)
+        self._lcount = torch.zeros(1, dtype=torch.int32, device=self.device)   # the fused loss's ticket word
         self._grads = True
 
     def draw_batch(self, i: Optional[int] = None):
@@ -785,21 +790,38 @@ class Trainer:
         table = self.embed_fn.table
         if rays.shape[0] == 0:
             return self._empty_rank_grads(batch)
-        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
-        if pf:
-            self._prefetch(i + 1)
         tv = mv = cubes = None
         if batch["tv"] is not None:
             cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
-        # loss value and its input gradients in one launch (the gradients do
-        # not depend on the value)
-        lo, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(
-            out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts, self._one)
+        # the loss fused into the forward (ABI 13): its gradients and the
+        # composite backward of both passes formed by the forward's waves,
+        # the value reduced by its last workgroup -- hn_loss_fwd_bwd and the
+        # backward's composite pre-pass do not run
+        fused_loss = self.fuse_loss and rays.shape[0] % 4 == 0
+        if fused_loss:
+            lo = torch.empty(4, dtype=torch.float32, device=self.device)
+            out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True,
+                                    loss=dict(target=target, tv=tv, world=self.world,
+                                              sparse_w=a.sparse_loss_weight, tv_w=a.tv_loss_weight, out=lo,
+                                              counter=self._lcount))
+            if pf:
+                self._prefetch(i + 1)
+            grads = {}
+            # d loss / d tv_l = g * tv_w with g = 1 (hn_loss_bwd's g_tv)
+            g_tv = None if tv is None else torch.full_like(tv, a.tv_loss_weight)
+        else:
+            out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
+            if pf:
+                self._prefetch(i + 1)
+            # loss value and its input gradients in one launch (the gradients do
+            # not depend on the value)
+            lo, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(
+                out["rgb"], out["rgb0"], target, out["sparsity"], out["sparsity0"], tv, *consts, self._one)
+            grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)
         # the ten MLP grads (one flat buffer) are written, not accumulated:
         # no zero fill
-        grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)
         # the TV term's table gradient joins the render backward (records of
         # the binned owner pass, or added to the stored gradient)
         tvb = None if tv is None else (mv, cubes, g_tv)
@@ -809,7 +831,7 @@ class Trainer:
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask())
+                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), draw_ready=fused_loss)
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
@@ -817,7 +839,7 @@ class Trainer:
             # DP exchange its owner pass runs per segment inside the exchange
             defer = self._xchg is not None and self._xchg.seg_bins is not None
             HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True, tv=tvb,
-                          owner_defer=defer)
+                          owner_defer=defer, draw_ready=fused_loss)
             self._owner_st = st if defer else None
             table.grad = self._gtable
         for p, g in zip(self._ws, self._gws):

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 12
+#define HN_ABI_VERSION 13
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -158,6 +158,26 @@ typedef struct hn_render_cfg {
 #define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the
                                          MLPs' ReLU masks of those points (ABI 10) */
 
+/* ABI 13: the training loss fused into hn_render_fwd (the trainer's step;
+ * replaces hn_loss_fwd_bwd + the backward's composite pre-pass).  The loss is
+ * run_nerf.py:612-636 under train.dp_loss's data-parallel rule:
+ *   loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * sum(entropy + entropy0)
+ *          + tv_w * sum(tv)
+ * With `loss` set the forward also forms its gradient w.r.t. both passes' rgb
+ * and entropy (hn_loss_bwd's op forms, g_loss = 1), runs the raw2outputs
+ * backward (run_nerf_helpers.py:577-628) of each ray and leaves d raw in the
+ * workspace for hn_render_bwd (draw_ready = 1, the same workspace), and
+ * reduces the loss value into out[4] = loss, mse, mse0, sum of entropies
+ * (hn_loss_fwd's fp64 sums, in another order).  n_rays a multiple of 4. */
+typedef struct hn_render_loss {
+  const float* target;      /* [B][3] */
+  const float* tv;          /* [n_tv] per-level TV values (hn_tv_fwd), or NULL */
+  int32_t n_tv;
+  float world, sparse_w, tv_w;
+  float* out;               /* [4] */
+  uint32_t* counter;        /* device word, 0 on entry and left 0: the last workgroup's ticket */
+} hn_render_loss;
+
 typedef struct hn_render_fwd_args {
   int64_t n_rays;
   const float* rays;        /* [B][11] = [o3 d3 near far viewdir3] (run_nerf_helpers.py:509-512) */
@@ -182,6 +202,7 @@ typedef struct hn_render_fwd_args {
   float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
                                evaluated points and their ReLU masks (MFMA-tile order,
                                opaque); NULL = not kept (inference); required by hn_render_bwd */
+  const hn_render_loss* loss;   /* ABI 13: NULL, or the fused training loss (above; needs feat) */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -236,6 +257,10 @@ typedef struct hn_render_bwd_args {
    * start each range's gradient exchange while the next range is reduced).
    * The workspace must not be touched in between. */
   int32_t owner_defer;
+  /* ABI 13: nonzero = the forward ran with `loss` on this workspace (weights_packed
+   * required): d raw is there already, the upstream g_* are not read, and the
+   * composite pre-pass is skipped. */
+  int32_t draw_ready;
 } hn_render_bwd_args;
 
 /* The binned scatter's bins for this cfg and batch: returns their number (0:

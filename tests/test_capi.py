@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(hn):
     for n in names:
         assert hasattr(lib, n), n
         assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
-    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 12
+    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 13
 
 
 def test_struct_sizes_match_header(hn):
@@ -49,7 +49,7 @@ def test_struct_layouts_match_compiled_header(hn, tmp_path):
                "hn_render_cfg": L.HnRenderCfg, "hn_render_fwd_args": L.HnRenderFwdArgs,
                "hn_render_bwd_args": L.HnRenderBwdArgs, "hn_tv_args": L.HnTvArgs,
                "hn_ray_sampler": L.HnRaySampler, "hn_ray_pool": L.HnRayPool,
-               "hn_radam_tensor": L.HnRadamTensor}
+               "hn_radam_tensor": L.HnRadamTensor, "hn_render_loss": L.HnRenderLoss}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hashnerf_amd.h"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')

@@ -258,3 +258,89 @@ def test_trainer_prefetch_same_trajectory(hn, batching):
     assert torch.equal(a[1], b[1])
     for x, y in zip(a[2], b[2]):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("world,tv", [(1, True), (2, False)])
+def test_fused_loss_forward_matches_separate(hn, world, tv):
+    """ABI 13: render_fwd(loss=...) forms the loss gradients and both passes'
+    composite backward inside the forward; render_bwd(draw_ready=True) then
+    skips its pre-pass.  Against render_fwd + hn_loss_fwd_bwd + render_bwd on
+    the same inputs (4096 rays, T=19, binned scatter): the forward outputs,
+    the table gradient and the ten MLP gradients are bitwise equal (d raw is:
+    the same composite backward on the same values); the loss value agrees
+    to 1e-6 (fp64 sums in another order).  world=2 applies the DP rule."""
+    from hashnerf_pytorch_amd import functional as HF
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(200, 200, 4, DEV, seed=0, scene="procedural")
+    args = default_args(N_rand=4096, log2_hashmap_size=19, tv_loss_weight=1e-3 if tv else 0.0,
+                        tv_until=10 ** 6, sparse_loss_weight=1e-3)
+    tr = Trainer(args, data, DEV, seed=1)
+    tr._fused_setup()
+    torch.manual_seed(3)
+    b = tr.draw_batch(600)
+    table = tr.embed_fn.table
+    tvv = mv = cubes = None
+    if b["tv"] is not None:
+        cubes, mv0 = b["tv"]
+        tvv, mv = HF.tv_fwd(table, mv0, cubes, tr.embed_fn.log2_hashmap_size)
+    consts = (world, args.sparse_loss_weight, args.tv_loss_weight)
+    # separate: forward, loss kernel, backward with its composite pre-pass
+    out_a, st_a = HF.render_fwd(tr._cfg, b["rays"], tr._t_vals, b["t_rand"], b["u"], None, None, table, tr._ws, True)
+    lo_a, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(out_a["rgb"], out_a["rgb0"], b["target"],
+                                                               out_a["sparsity"], out_a["sparsity0"], tvv, *consts,
+                                                               torch.ones((), device=DEV))
+    dt_a = torch.empty_like(table)
+    dw_a = HF.zeros_like_all(tr._ws)
+    tvb = None if tvv is None else (mv, cubes, g_tv)
+    HF.render_bwd(st_a, dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0), dt_a, dw_a,
+                  overwrite=True, overwrite_mlp=True, tv=tvb)
+    # fused
+    lo_b = torch.empty(4, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out_b, st_b = HF.render_fwd(tr._cfg, b["rays"], tr._t_vals, b["t_rand"], b["u"], None, None, table, tr._ws,
+                                True, loss=dict(target=b["target"], tv=tvv, world=world,
+                                                sparse_w=args.sparse_loss_weight, tv_w=args.tv_loss_weight,
+                                                out=lo_b, counter=cnt))
+    dt_b = torch.empty_like(table)
+    dw_b = HF.zeros_like_all(tr._ws)
+    tvb = None if tvv is None else (mv, cubes, torch.full_like(tvv, args.tv_loss_weight))
+    HF.render_bwd(st_b, {}, dt_b, dw_b, overwrite=True, overwrite_mlp=True, tv=tvb, draw_ready=True)
+    torch.cuda.synchronize()
+    HF.L.check_device_faults()
+    for k in ("rgb", "rgb0", "depth", "acc", "sparsity", "sparsity0", "z_fine", "raw_f"):
+        assert torch.equal(out_a[k], out_b[k]), k
+    if tvv is not None:
+        assert torch.equal(g_tv, torch.full_like(tvv, args.tv_loss_weight))
+    assert int(cnt.item()) == 0, "the ticket word must be left 0 for the next launch"
+    torch.testing.assert_close(lo_b, lo_a, rtol=1e-6, atol=0)
+    assert torch.equal(dt_a, dt_b)
+    for x, y in zip(dw_a, dw_b):
+        assert torch.equal(x, y)
+
+
+def test_trainer_fused_loss_same_trajectory(hn):
+    """Trainer.fuse_loss (ABI 13, the default) against the separate loss
+    kernel + composite pre-pass: 8 steps (TV through step 5, the fused table
+    step) leave table, moments and MLP weights bitwise equal; the losses agree
+    to 1e-6."""
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
+    res = {}
+    for fl in (False, True):
+        args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=5,
+                            sparse_loss_weight=1e-3)
+        tr = Trainer(args, data, DEV, seed=3)
+        tr.fuse_loss = fl
+        torch.manual_seed(11)
+        losses = [float(tr.step()[0]) for _ in range(8)]
+        t = tr.embed_fn.table
+        st = tr.optimizer.state[t]
+        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+        res[fl] = (losses, t.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(),
+                   [p.detach().clone() for p in ws])
+    a, b = res[False], res[True]
+    np.testing.assert_allclose(b[0], a[0], rtol=1e-6)
+    for k in (1, 2, 3):
+        assert torch.equal(a[k], b[k]), k
+    for x, y in zip(a[4], b[4]):
+        assert torch.equal(x, y)
