@@ -50,7 +50,7 @@ _P = C.c_void_p
 
 class HnRenderLoss(C.Structure):
     _fields_ = [("target", _P), ("tv", _P), ("n_tv", C.c_int32), ("world", C.c_float), ("sparse_w", C.c_float),
-                ("tv_w", C.c_float), ("out", _P), ("counter", _P)]
+                ("tv_w", C.c_float), ("out", _P), ("counter", _P), ("g_rgb", _P), ("g_rgb0", _P)]
 
 
 class HnRenderFwdArgs(C.Structure):
@@ -78,8 +78,7 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
                 ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
-                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32),
-                ("draw_ready", C.c_int32)]
+                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32)]
 
 
 class HnTvArgs(C.Structure):

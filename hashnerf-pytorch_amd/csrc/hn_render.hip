@@ -62,11 +62,11 @@ struct RenderK {
   uint8_t* fine_src;
   float* feat;    // [B][8 tiles][1024] saved features or NULL
   // ABI 13 fused training loss (hn_render_loss; target NULL = none): the
-  // composite backward of both passes into draw, the loss value reduced by
-  // the last workgroup from per-workgroup fp64 partials
+  // loss gradients w.r.t. both passes' rgb, the loss value reduced by the
+  // last workgroup from per-workgroup fp64 partials
   const float* target;
-  float lgm, lsparse;   // (g / world) / (3 B) and g * sparse_w with g = 1: hn_loss_bwd's op forms
-  float* draw;          // [B][64 + 192][4] (the backward's pre-pass output, in the workspace)
+  float lgm;            // (g / world) / (3 B) with g = 1: hn_loss_bwd's op forms
+  float *g_rgb, *g_rgb0;
   double* lpart;        // [workgroups][4] (in the workspace's dW-slab region, free until the backward)
   uint32_t* lcount;
   const float* ltv;
@@ -100,7 +100,6 @@ struct B1K {
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   float* dfeat_f;       // split backward: [B][6 fine tiles][1024] fine-pass feature grads (tile order)
-  int32_t zero_book;    // ABI 13 draw_ready: the MLP-backward kernel resets the overflow book
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -418,26 +417,13 @@ void render_fwd_kernel(RenderK k) {
   }
   double l_se0 = 0.0;   // fused loss: this ray's squared errors (coarse, fine)
   if (k.target) {
-    // d loss / d rgb0, d loss / d entropy0 (hn_loss_bwd_elem's op forms), then
-    // the coarse raw2outputs backward in place over rawb (free until the
-    // merge sort below uses it as scratch): render_comp_bwd_kernel's values
-    CompGrad g;
-    g.has_rgb = g.has_entropy = true;
-    g.has_acc = g.has_depth = false;
-    g.acc = g.depth = 0.f;
+    // d loss / d rgb0 (hn_loss_bwd_elem's op forms, g_loss = 1)
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float e = co.rgb[c] - k.target[3 * ray + c];
-      g.rgb[c] = k.lgm * (2.f * e);
+      if (lane == c) k.g_rgb0[3 * ray + c] = k.lgm * (2.f * e);
       l_se0 += (double)(e * e);
     }
-    g.entropy = k.lsparse;
-    composite_bwd<1>(rawb, zc, k.noise_c ? k.noise_c + ray * kSc : nullptr, kSc, r.dnorm, k.white != 0, g,
-                     nullptr, nullptr, rawb, lane);
-    lds_fence_wave();
-    *reinterpret_cast<float4*>(k.draw + ((size_t)ray * (kSc + kSf) + lane) * 4) =
-        *reinterpret_cast<const float4*>(rawb + 4 * lane);
-    lds_fence_wave();
   }
 
   // ---- importance sampling (:547-551) ----
@@ -517,24 +503,13 @@ void render_fwd_kernel(RenderK k) {
     k.sparsity[ray] = fo.entropy;
   }
   if (k.target) {
-    CompGrad g;
-    g.has_rgb = g.has_entropy = true;
-    g.has_acc = g.has_depth = false;
-    g.acc = g.depth = 0.f;
     double l_se = 0.0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float e = fo.rgb[c] - k.target[3 * ray + c];
-      g.rgb[c] = k.lgm * (2.f * e);
+      if (lane == c) k.g_rgb[3 * ray + c] = k.lgm * (2.f * e);
       l_se += (double)(e * e);
     }
-    g.entropy = k.lsparse;
-    lds_fence_wave();   // the composite's reads of rawb are done (in-order LDS; compiler order)
-    composite_bwd<3>(rawb, zs, k.noise_f ? k.noise_f + ray * kSf : nullptr, kSf, r.dnorm, k.white != 0, g,
-                     nullptr, nullptr, rawb, lane);
-    lds_fence_wave();
-    float4* dst = reinterpret_cast<float4*>(k.draw + ((size_t)ray * (kSc + kSf) + kSc) * 4);
-    for (int j = lane; j < kSf; j += 64) dst[j] = *reinterpret_cast<const float4*>(rawb + 4 * j);
     loss_partials(k, l_se, l_se0, (double)fo.entropy + (double)co.entropy, wave, lane);
   }
 #if HN_PROFILE
@@ -2608,7 +2583,6 @@ void render_bwd_kernel(B1K k) {
   int* sync = reinterpret_cast<int*>(gsl + kGsLds);
   stage_grid_sizes(k.g, gsl);
   if (threadIdx.x < kSyncInts) sync[threadIdx.x] = 0;
-  if (k.zero_book && blockIdx.x == 0) zero_ovf_book(k);   // no composite pre-pass ran (draw_ready)
   __syncthreads();
   const Ring ring{slots, &sync[2], &sync[5], &sync[5 + kSlots], gsl};
   const int64_t nb = gridDim.x;
@@ -3181,22 +3155,21 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
   k.target = nullptr;
-  k.draw = nullptr; k.lpart = nullptr; k.lcount = nullptr; k.ltv = nullptr; k.lout = nullptr;
+  k.g_rgb = k.g_rgb0 = nullptr; k.lpart = nullptr; k.lcount = nullptr; k.ltv = nullptr; k.lout = nullptr;
   k.n_tv = 0;
-  k.lgm = k.lsparse = k.world = k.sparse_w = k.tv_w = 0.f;
+  k.lgm = k.world = k.sparse_w = k.tv_w = 0.f;
   if (a->loss) {   // ABI 13: the training loss fused in (hn_render_loss)
     const hn_render_loss& L = *a->loss;
-    if (!L.target || !L.out || !L.counter || !a->feat || (L.n_tv && !L.tv)) return HN_E_NULL;
+    if (!L.target || !L.out || !L.counter || !L.g_rgb || !L.g_rgb0 || (L.n_tv && !L.tv)) return HN_E_NULL;
     if (a->n_rays % kFwdBlockWaves || L.n_tv < 0 || L.n_tv > 64 || !(L.world > 0.f)) return HN_E_SHAPE;
     k.target = L.target;
-    // hn_loss_bwd's upstream factors with g_loss = 1: (g / world) / (3 n), g * sparse_w
+    // hn_loss_bwd's upstream factor with g_loss = 1: (g / world) / (3 n)
     const float g = 1.f;
     k.lgm = (g / L.world) / (float)(3 * a->n_rays);
-    k.lsparse = g * L.sparse_w;
-    // the backward's d raw region and, for the partials, the dW slabs (written by the backward later)
-    float* slab = Pf + G_END;
-    k.lpart = reinterpret_cast<double*>(slab);
-    k.draw = slab + (size_t)kBwdBlocks * kSlabSlots * W_END + (size_t)a->n_rays * kDcRay;
+    k.g_rgb = L.g_rgb;
+    k.g_rgb0 = L.g_rgb0;
+    // the partials in the dW slabs of the workspace (written by a backward later)
+    k.lpart = reinterpret_cast<double*>(Pf + G_END);
     k.lcount = L.counter;
     k.ltv = L.n_tv ? L.tv : nullptr;
     k.n_tv = L.n_tv;
@@ -3285,7 +3258,6 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     return HN_E_NULL;
   if ((!a->d_table && !a->table_step) || !grad_ok(a->d_coarse) || !grad_ok(a->d_fine)) return HN_E_NULL;
   if (a->d_table_mode < 0 || a->d_table_mode > 3) return HN_E_SHAPE;
-  if (a->draw_ready && !a->weights_packed) return HN_E_SHAPE;   // d raw lives in the forward's workspace
   if (!workspace) return HN_E_NULL;
   if (ws_bytes < hn_render_workspace_bytes(cfg, a->n_rays)) return HN_E_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -3359,12 +3331,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     const size_t tb = ((size_t)16 << T) * 2 * sizeof(float);
     if ((st = hip_status(hipMemsetAsync(a->d_table, 0, tb, s)))) return st;
   }
-  k.zero_book = 0;
-  if (!a->draw_ready)
-    hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
-                       dim3(64 * kFwdWaves), 0, s, k);
-  else
-    k.zero_book = k.bins != nullptr;   // the pre-pass's other duty moves to the MLP-backward kernel
+  hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
+                     dim3(64 * kFwdWaves), 0, s, k);
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
   if (mode == kModeSplit)

@@ -226,11 +226,12 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     output dict and a RenderState (None when keep_feat is False).
 
     loss (ABI 13, the trainer's step): dict(target [B, 3], tv [L] or None,
-    world, sparse_w, tv_w, out [4] device, counter [1] int32 device zero)
-    fuses the training loss (run_nerf.py:612-636 under train.dp_loss's rule)
-    into the forward: out = loss, mse, mse0, entropy sum (loss_fwd's), and
-    the composite backward of both passes is left in the workspace -- pass
-    draw_ready=True to render_bwd (its g_* are then not used).  B % 4 == 0."""
+    world, sparse_w, tv_w, out [4] device, counter [1] int32 device zero,
+    g_rgb / g_rgb0 [B, 3] device outputs) fuses the training loss
+    (run_nerf.py:612-636 under train.dp_loss's rule) into the forward: out =
+    loss, mse, mse0, entropy sum (loss_fwd's), g_rgb / g_rgb0 = its gradient
+    w.r.t. rgb / rgb0 (loss_bwd's; the entropy and TV gradients are the
+    constants sparse_w and tv_w).  B % 4 == 0."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -259,8 +260,6 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     a.feat = feat.data_ptr() if keep_feat else None
     keep_loss = None
     if loss is not None:
-        if not keep_feat:
-            raise ValueError("hashnerf_amd.render_fwd: a fused loss needs keep_feat (its backward follows)")
         la = L.HnRenderLoss()
         tgt = L.contig(loss["target"])
         tv = loss.get("tv")
@@ -270,6 +269,8 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
         la.n_tv = 0 if tv is None else tv.numel()
         la.world, la.sparse_w, la.tv_w = float(loss["world"]), float(loss["sparse_w"]), float(loss["tv_w"])
         la.out, la.counter = loss["out"].data_ptr(), loss["counter"].data_ptr()
+        L.require_device(loss["g_rgb"], loss["g_rgb0"])
+        la.g_rgb, la.g_rgb0 = loss["g_rgb"].data_ptr(), loss["g_rgb0"].data_ptr()
         a.loss = C.pointer(la)
         keep_loss = (la, tgt, tv)
     nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
@@ -290,8 +291,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
 
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
-               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False,
-               draw_ready: bool = False):
+               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -363,8 +363,6 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
         keep.append(g_tv)
         a.g_tv = g_tv.data_ptr()
     a.owner_defer = 1 if owner_defer else 0
-    # draw_ready: the forward ran with its fused loss on this workspace (ABI 13)
-    a.draw_ready = 1 if draw_ready else 0
     t0 = TIMER.begin("render_bwd")
     L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
     TIMER.end("render_bwd", t0)

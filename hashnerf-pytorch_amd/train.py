@@ -577,9 +577,9 @@ class Trainer:
         # unless asked for (bench.py --prefetch).
         self.prefetch = False
         self._pf = None          # (step, batch, ready event) drawn ahead
-        # explicit mode: the loss, its gradients and the composite backward
-        # fused into the render forward (ABI 13; batches of a multiple of 4
-        # rays) instead of hn_loss_fwd_bwd + the backward's composite pre-pass
+        # explicit mode: the loss value and its rgb gradients fused into the
+        # render forward (ABI 13; batches of a multiple of 4 rays) instead of
+        # an hn_loss_fwd_bwd launch
         self.fuse_loss = True
         self._side = None
 
@@ -723,6 +723,7 @@ class Trainer:
         self._gws = HF.zeros_like_all(self._ws)
         self._one = torch.ones((), device=self.device)
         self._lcount = torch.zeros(1, dtype=torch.int32, device=self.device)   # the fused loss's ticket word
+        self._gsp = None
         self._grads = True
 
     def draw_batch(self, i: Optional[int] = None):
@@ -795,21 +796,26 @@ class Trainer:
             cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
-        # the loss fused into the forward (ABI 13): its gradients and the
-        # composite backward of both passes formed by the forward's waves,
-        # the value reduced by its last workgroup -- hn_loss_fwd_bwd and the
-        # backward's composite pre-pass do not run
-        fused_loss = self.fuse_loss and rays.shape[0] % 4 == 0
+        # the loss fused into the forward (ABI 13): its gradient w.r.t. rgb /
+        # rgb0 written by the forward's waves, the value reduced by its last
+        # workgroup -- no hn_loss_fwd_bwd launch
+        B = rays.shape[0]
+        fused_loss = self.fuse_loss and B % 4 == 0
         if fused_loss:
             lo = torch.empty(4, dtype=torch.float32, device=self.device)
+            g_rgb = torch.empty((B, 3), dtype=torch.float32, device=self.device)
+            g_rgb0 = torch.empty((B, 3), dtype=torch.float32, device=self.device)
             out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True,
                                     loss=dict(target=target, tv=tv, world=self.world,
                                               sparse_w=a.sparse_loss_weight, tv_w=a.tv_loss_weight, out=lo,
-                                              counter=self._lcount))
+                                              counter=self._lcount, g_rgb=g_rgb, g_rgb0=g_rgb0))
             if pf:
                 self._prefetch(i + 1)
-            grads = {}
-            # d loss / d tv_l = g * tv_w with g = 1 (hn_loss_bwd's g_tv)
+            # d loss / d entropy = g * sparse_w, d loss / d tv_l = g * tv_w with
+            # g = 1 (hn_loss_bwd's): constants
+            if self._gsp is None or self._gsp.shape[0] != B:
+                self._gsp = torch.full((B,), a.sparse_loss_weight, dtype=torch.float32, device=self.device)
+            grads = dict(g_rgb=g_rgb, g_sparsity=self._gsp, g_rgb0=g_rgb0, g_sparsity0=self._gsp)
             g_tv = None if tv is None else torch.full_like(tv, a.tv_loss_weight)
         else:
             out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
@@ -831,7 +837,7 @@ class Trainer:
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), draw_ready=fused_loss)
+                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask())
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
@@ -839,7 +845,7 @@ class Trainer:
             # DP exchange its owner pass runs per segment inside the exchange
             defer = self._xchg is not None and self._xchg.seg_bins is not None
             HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True, tv=tvb,
-                          owner_defer=defer, draw_ready=fused_loss)
+                          owner_defer=defer)
             self._owner_st = st if defer else None
             table.grad = self._gtable
         for p, g in zip(self._ws, self._gws):

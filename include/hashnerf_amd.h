@@ -159,16 +159,15 @@ typedef struct hn_render_cfg {
                                          MLPs' ReLU masks of those points (ABI 10) */
 
 /* ABI 13: the training loss fused into hn_render_fwd (the trainer's step;
- * replaces hn_loss_fwd_bwd + the backward's composite pre-pass).  The loss is
- * run_nerf.py:612-636 under train.dp_loss's data-parallel rule:
+ * replaces its hn_loss_fwd_bwd launch).  The loss is run_nerf.py:612-636
+ * under train.dp_loss's data-parallel rule:
  *   loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * sum(entropy + entropy0)
  *          + tv_w * sum(tv)
- * With `loss` set the forward also forms its gradient w.r.t. both passes' rgb
- * and entropy (hn_loss_bwd's op forms, g_loss = 1), runs the raw2outputs
- * backward (run_nerf_helpers.py:577-628) of each ray and leaves d raw in the
- * workspace for hn_render_bwd (draw_ready = 1, the same workspace), and
- * reduces the loss value into out[4] = loss, mse, mse0, sum of entropies
- * (hn_loss_fwd's fp64 sums, in another order).  n_rays a multiple of 4. */
+ * With `loss` set the forward also writes its gradient w.r.t. both passes'
+ * rgb (hn_loss_bwd's op forms, g_loss = 1; the entropy and TV gradients are
+ * the constants sparse_w and tv_w) and reduces the loss value into out[4] =
+ * loss, mse, mse0, sum of entropies (hn_loss_fwd's fp64 sums, in another
+ * order).  n_rays a multiple of 4. */
 typedef struct hn_render_loss {
   const float* target;      /* [B][3] */
   const float* tv;          /* [n_tv] per-level TV values (hn_tv_fwd), or NULL */
@@ -176,6 +175,8 @@ typedef struct hn_render_loss {
   float world, sparse_w, tv_w;
   float* out;               /* [4] */
   uint32_t* counter;        /* device word, 0 on entry and left 0: the last workgroup's ticket */
+  float* g_rgb;             /* [B][3] d loss / d rgb (hn_render_bwd's g_rgb) */
+  float* g_rgb0;            /* [B][3] d loss / d rgb0 */
 } hn_render_loss;
 
 typedef struct hn_render_fwd_args {
@@ -202,7 +203,7 @@ typedef struct hn_render_fwd_args {
   float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
                                evaluated points and their ReLU masks (MFMA-tile order,
                                opaque); NULL = not kept (inference); required by hn_render_bwd */
-  const hn_render_loss* loss;   /* ABI 13: NULL, or the fused training loss (above; needs feat) */
+  const hn_render_loss* loss;   /* ABI 13: NULL, or the fused training loss (above) */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -257,10 +258,6 @@ typedef struct hn_render_bwd_args {
    * start each range's gradient exchange while the next range is reduced).
    * The workspace must not be touched in between. */
   int32_t owner_defer;
-  /* ABI 13: nonzero = the forward ran with `loss` on this workspace (weights_packed
-   * required): d raw is there already, the upstream g_* are not read, and the
-   * composite pre-pass is skipped. */
-  int32_t draw_ready;
 } hn_render_bwd_args;
 
 /* The binned scatter's bins for this cfg and batch: returns their number (0:
