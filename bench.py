@@ -304,6 +304,8 @@ def main():
                          "the owner pass has formed it (1: one exchange after the backward)")
     ap.add_argument("--prefetch", action="store_true",
                     help="A/B: draw the next step's batch on a side stream beside the backward")
+    ap.add_argument("--separate-loss", action="store_true",
+                    help="A/B: the loss in its own hn_loss_fwd_bwd launch instead of the backward's pre-pass")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -367,6 +369,7 @@ def main():
     # measured slower (r05k: 0.996 vs 0.982 ms per step) -- the cross-stream
     # waits cost more than the ~20 us of sampler and RNG launches they move
     tr.prefetch = args.prefetch
+    tr.fuse_loss = not args.separate_loss
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1

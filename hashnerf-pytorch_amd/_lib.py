@@ -49,8 +49,9 @@ _P = C.c_void_p
 
 
 class HnRenderLoss(C.Structure):
-    _fields_ = [("target", _P), ("tv", _P), ("n_tv", C.c_int32), ("world", C.c_float), ("sparse_w", C.c_float),
-                ("tv_w", C.c_float), ("out", _P), ("counter", _P), ("g_rgb", _P), ("g_rgb0", _P)]
+    _fields_ = [("target", _P), ("rgb", _P), ("rgb0", _P), ("sparsity", _P), ("sparsity0", _P), ("tv", _P),
+                ("n_tv", C.c_int32), ("world", C.c_float), ("sparse_w", C.c_float), ("tv_w", C.c_float),
+                ("out", _P)]
 
 
 class HnRenderFwdArgs(C.Structure):
@@ -59,7 +60,7 @@ class HnRenderFwdArgs(C.Structure):
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
                 ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
-                ("fine_src", _P), ("feat", _P), ("loss", C.POINTER(HnRenderLoss))]
+                ("fine_src", _P), ("feat", _P)]
 
 
 class HnRadamTensor(C.Structure):
@@ -78,7 +79,8 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_rgb0", _P), ("g_depth0", _P), ("g_acc0", _P), ("g_sparsity0", _P),
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
                 ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
-                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32)]
+                ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32),
+                ("loss", C.POINTER(HnRenderLoss))]
 
 
 class HnTvArgs(C.Structure):

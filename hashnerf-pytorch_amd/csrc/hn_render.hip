@@ -16,6 +16,7 @@
 // backward + float atomics into the hash-table gradient.
 #include "hn_mlp.h"
 #include "hn_render.h"
+#include "hn_loss.h"
 #include "hn_tv.h"
 
 #include <math.h>
@@ -61,18 +62,6 @@ struct RenderK {
   float *z_coarse, *z_fine, *raw_c, *raw_f;
   uint8_t* fine_src;
   float* feat;    // [B][8 tiles][1024] saved features or NULL
-  // ABI 13 fused training loss (hn_render_loss; target NULL = none): the
-  // loss gradients w.r.t. both passes' rgb, the loss value reduced by the
-  // last workgroup from per-workgroup fp64 partials
-  const float* target;
-  float lgm;            // (g / world) / (3 B) with g = 1: hn_loss_bwd's op forms
-  float *g_rgb, *g_rgb0;
-  double* lpart;        // [workgroups][4] (in the workspace's dW-slab region, free until the backward)
-  uint32_t* lcount;
-  const float* ltv;
-  int32_t n_tv;
-  float world, sparse_w, tv_w;
-  float* lout;
 };
 
 
@@ -100,6 +89,12 @@ struct B1K {
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   float* dfeat_f;       // split backward: [B][6 fine tiles][1024] fine-pass feature grads (tile order)
+  // ABI 13 training loss formed by the composite pre-pass (hn_render_loss;
+  // lout NULL = none): hn_loss_bwd's upstream factors (g = 1), the value's inputs
+  const float *ltarget, *lrgb, *lrgb0, *lsp, *lsp0, *ltv;
+  int32_t n_tv;
+  float lgm, lsparse, lworld, lsparse_w, ltv_w;
+  float* lout;
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -265,62 +260,6 @@ __device__ unsigned long long g_fwd_prof[8];
 // 0.301-0.313 ms; profiles/r04/r04e, r04f.)
 constexpr int kFwdBlockWaves = kFwdWaves;
 
-// Fused loss value: the workgroup's fp64 partials (squared errors fine and
-// coarse, entropy sums; wave order fixed), then the last workgroup to finish
-// (ticket from an agent-scope counter, released / acquired as
-// MI355X_MICROARCH.md's hand-off recipe prescribes) sums every workgroup's
-// partials in a fixed order and writes hn_loss_fwd's out[4]; it resets the
-// counter for the next launch.  Every wave of the workgroup calls this.
-HN_DEV void loss_partials(const RenderK& k, double se, double se0, double ent, int wave, int lane) {
-  __shared__ double lp[kFwdBlockWaves][3];
-  __shared__ uint32_t last;
-  if (lane == 0) {
-    lp[wave][0] = se;
-    lp[wave][1] = se0;
-    lp[wave][2] = ent;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t[3] = {0.0, 0.0, 0.0};
-    for (int w = 0; w < kFwdBlockWaves; ++w)
-      for (int q = 0; q < 3; ++q) t[q] += lp[w][q];
-    for (int q = 0; q < 3; ++q) k.lpart[4 * (size_t)blockIdx.x + q] = t[q];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t tk = __hip_atomic_fetch_add(k.lcount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = tk == gridDim.x - 1 ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  double a[3] = {0.0, 0.0, 0.0};
-  for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x)
-    for (int q = 0; q < 3; ++q) a[q] += k.lpart[4 * (size_t)b + q];
-  for (int q = 0; q < 3; ++q) a[q] = wave_sum(a[q]);
-  __syncthreads();   // lp is read again below
-  if (lane == 0)
-    for (int q = 0; q < 3; ++q) lp[wave][q] = a[q];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int w = 0; w < kFwdBlockWaves; ++w)
-      for (int q = 0; q < 3; ++q) t[q] += lp[w][q];
-    for (int j = 0; j < k.n_tv; ++j) t[3] += (double)k.ltv[j];
-    // hn_loss_fwd's value (loss_fwd_block)
-    const double N = 3.0 * (double)k.B;
-    const float mse = (float)(t[0] / N), mse0 = (float)(t[1] / N);
-    const float ent = (float)t[2];
-    k.lout[0] = (mse + mse0) / k.world + k.sparse_w * ent + (k.ltv ? k.tv_w * (float)t[3] : 0.f);
-    k.lout[1] = mse;
-    k.lout[2] = mse0;
-    k.lout[3] = ent;
-    *k.lcount = 0u;
-  }
-}
 
 __global__ __launch_bounds__(64 * kFwdBlockWaves)
 __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
@@ -415,16 +354,6 @@ void render_fwd_kernel(RenderK k) {
     k.acc0[ray] = co.acc;
     k.sparsity0[ray] = co.entropy;
   }
-  double l_se0 = 0.0;   // fused loss: this ray's squared errors (coarse, fine)
-  if (k.target) {
-    // d loss / d rgb0 (hn_loss_bwd_elem's op forms, g_loss = 1)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float e = co.rgb[c] - k.target[3 * ray + c];
-      if (lane == c) k.g_rgb0[3 * ray + c] = k.lgm * (2.f * e);
-      l_se0 += (double)(e * e);
-    }
-  }
 
   // ---- importance sampling (:547-551) ----
   if (lane < kSc - 1) bins[lane] = .5f * (zc[lane + 1] + zc[lane]);
@@ -501,16 +430,6 @@ void render_fwd_kernel(RenderK k) {
     k.depth[ray] = fo.depth;
     k.acc[ray] = fo.acc;
     k.sparsity[ray] = fo.entropy;
-  }
-  if (k.target) {
-    double l_se = 0.0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float e = fo.rgb[c] - k.target[3 * ray + c];
-      if (lane == c) k.g_rgb[3 * ray + c] = k.lgm * (2.f * e);
-      l_se += (double)(e * e);
-    }
-    loss_partials(k, l_se, l_se0, (double)fo.entropy + (double)co.entropy, wave, lane);
   }
 #if HN_PROFILE
   HN_FT(5);
@@ -2452,6 +2371,10 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0) zero_ovf_book(k);   // binned scatter: no overflow records yet
+  // the loss value (hn_loss_fwd's reduction) by workgroup 0, beside its rays
+  if (k.lout && blockIdx.x == 0)
+    loss_fwd_block<64 * kFwdWaves>(k.lrgb, k.lrgb0, k.ltarget, k.lsp, k.lsp0, k.B, k.ltv, k.n_tv, k.lworld,
+                                   k.lsparse_w, k.ltv_w, k.lout);
   const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
   const int64_t ray = w >> 1;
@@ -2473,15 +2396,25 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const float* gacc = fine ? k.g_acc : k.g_acc0;
   const float* gdep = fine ? k.g_depth : k.g_depth0;
   const float* gent = fine ? k.g_sparsity : k.g_sparsity0;
-  g.has_rgb = grgb != nullptr;
-  g.has_acc = gacc != nullptr;
-  g.has_depth = gdep != nullptr;
-  g.has_entropy = gent != nullptr;
+  if (k.lout) {   // the training loss's gradients (hn_loss_bwd_elem's op forms, g_loss = 1)
+    const float* x = fine ? k.lrgb : k.lrgb0;
+    g.has_rgb = g.has_entropy = true;
+    g.has_acc = g.has_depth = false;
 #pragma unroll
-  for (int c = 0; c < 3; ++c) g.rgb[c] = g.has_rgb ? grgb[3 * ray + c] : 0.f;
-  g.acc = g.has_acc ? gacc[ray] : 0.f;
-  g.depth = g.has_depth ? gdep[ray] : 0.f;
-  g.entropy = g.has_entropy ? gent[ray] : 0.f;
+    for (int c = 0; c < 3; ++c) g.rgb[c] = k.lgm * (2.f * (x[3 * ray + c] - k.ltarget[3 * ray + c]));
+    g.acc = g.depth = 0.f;
+    g.entropy = k.lsparse;
+  } else {
+    g.has_rgb = grgb != nullptr;
+    g.has_acc = gacc != nullptr;
+    g.has_depth = gdep != nullptr;
+    g.has_entropy = gent != nullptr;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) g.rgb[c] = g.has_rgb ? grgb[3 * ray + c] : 0.f;
+    g.acc = g.has_acc ? gacc[ray] : 0.f;
+    g.depth = g.has_depth ? gdep[ray] : 0.f;
+    g.entropy = g.has_entropy ? gent[ray] : 0.f;
+  }
   const float* noise = fine ? (k.noise_f ? k.noise_f + ray * S : nullptr)
                             : (k.noise_c ? k.noise_c + ray * S : nullptr);
   const float* graw = (fine && k.g_raw_f) ? k.g_raw_f + ray * S * 4 : nullptr;
@@ -3154,32 +3087,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.rgb0 = a->rgb0; k.depth0 = a->depth0; k.acc0 = a->acc0; k.sparsity0 = a->sparsity0;
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
-  k.target = nullptr;
-  k.g_rgb = k.g_rgb0 = nullptr; k.lpart = nullptr; k.lcount = nullptr; k.ltv = nullptr; k.lout = nullptr;
-  k.n_tv = 0;
-  k.lgm = k.world = k.sparse_w = k.tv_w = 0.f;
-  if (a->loss) {   // ABI 13: the training loss fused in (hn_render_loss)
-    const hn_render_loss& L = *a->loss;
-    if (!L.target || !L.out || !L.counter || !L.g_rgb || !L.g_rgb0 || (L.n_tv && !L.tv)) return HN_E_NULL;
-    if (a->n_rays % kFwdBlockWaves || L.n_tv < 0 || L.n_tv > 64 || !(L.world > 0.f)) return HN_E_SHAPE;
-    k.target = L.target;
-    // hn_loss_bwd's upstream factor with g_loss = 1: (g / world) / (3 n)
-    const float g = 1.f;
-    k.lgm = (g / L.world) / (float)(3 * a->n_rays);
-    k.g_rgb = L.g_rgb;
-    k.g_rgb0 = L.g_rgb0;
-    // the partials in the dW slabs of the workspace (written by a backward later)
-    k.lpart = reinterpret_cast<double*>(Pf + G_END);
-    k.lcount = L.counter;
-    k.ltv = L.n_tv ? L.tv : nullptr;
-    k.n_tv = L.n_tv;
-    k.world = L.world; k.sparse_w = L.sparse_w; k.tv_w = L.tv_w;
-    k.lout = L.out;
-  }
   const unsigned blocks = (unsigned)((a->n_rays + kFwdBlockWaves - 1) / kFwdBlockWaves);
-  static_assert((size_t)kBwdBlocks * kSlabSlots * W_END * 4 >= (size_t)(1 << 20) * 32,
-                "the loss partials of up to 2^20 workgroups fit the dW-slab region");
-  if (a->loss && blocks > (1u << 20)) return HN_E_SHAPE;
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdBlockWaves), 0, s, k);
 #if HN_PROFILE
   {
@@ -3286,6 +3194,24 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.slab = slab;
   k.dfeat = dfeat;
   k.draw = draw;
+  k.ltarget = k.lrgb = k.lrgb0 = k.lsp = k.lsp0 = k.ltv = nullptr;
+  k.n_tv = 0;
+  k.lgm = k.lsparse = k.lworld = k.lsparse_w = k.ltv_w = 0.f;
+  k.lout = nullptr;
+  if (a->loss) {   // ABI 13: the training loss formed by the pre-pass (hn_render_loss)
+    const hn_render_loss& L = *a->loss;
+    if (!L.target || !L.rgb || !L.rgb0 || !L.sparsity || !L.sparsity0 || !L.out || (L.n_tv && !L.tv))
+      return HN_E_NULL;
+    if (L.n_tv < 0 || !(L.world > 0.f)) return HN_E_SHAPE;
+    const float g = 1.f;   // hn_loss_bwd's factors with g_loss = 1
+    k.lgm = (g / L.world) / (float)(3 * a->n_rays);
+    k.lsparse = g * L.sparse_w;
+    k.ltarget = L.target; k.lrgb = L.rgb; k.lrgb0 = L.rgb0; k.lsp = L.sparsity; k.lsp0 = L.sparsity0;
+    k.ltv = L.n_tv ? L.tv : nullptr;
+    k.n_tv = L.n_tv;
+    k.lworld = L.world; k.lsparse_w = L.sparse_w; k.ltv_w = L.tv_w;
+    k.lout = L.out;
+  }
   k.g = make_grid_args(cfg->grid);
   k.fine_src = a->fine_src;
   k.d_table = a->d_table;

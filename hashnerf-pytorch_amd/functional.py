@@ -221,17 +221,9 @@ class RenderState:
                  "fine_src", "feat", "wsb", "nbytes", "bwd_args")
 
 
-def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, loss=None):
+def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat):
     """hn_render_fwd (run_nerf_helpers.py:464-574, forward).  Returns the
-    output dict and a RenderState (None when keep_feat is False).
-
-    loss (ABI 13, the trainer's step): dict(target [B, 3], tv [L] or None,
-    world, sparse_w, tv_w, out [4] device, counter [1] int32 device zero,
-    g_rgb / g_rgb0 [B, 3] device outputs) fuses the training loss
-    (run_nerf.py:612-636 under train.dp_loss's rule) into the forward: out =
-    loss, mse, mse0, entropy sum (loss_fwd's), g_rgb / g_rgb0 = its gradient
-    w.r.t. rgb / rgb0 (loss_bwd's; the entropy and TV gradients are the
-    constants sparse_w and tv_w).  B % 4 == 0."""
+    output dict and a RenderState (None when keep_feat is False)."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -258,21 +250,6 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     feat = torch.empty((B, L.RENDER_FEAT_PER_RAY) if keep_feat else (0,), dtype=torch.float32,
                        device=dev)
     a.feat = feat.data_ptr() if keep_feat else None
-    keep_loss = None
-    if loss is not None:
-        la = L.HnRenderLoss()
-        tgt = L.contig(loss["target"])
-        tv = loss.get("tv")
-        tv = L.contig(tv) if tv is not None else None
-        L.require_device(tgt, tv, loss["out"])
-        la.target, la.tv = tgt.data_ptr(), (tv.data_ptr() if tv is not None else None)
-        la.n_tv = 0 if tv is None else tv.numel()
-        la.world, la.sparse_w, la.tv_w = float(loss["world"]), float(loss["sparse_w"]), float(loss["tv_w"])
-        la.out, la.counter = loss["out"].data_ptr(), loss["counter"].data_ptr()
-        L.require_device(loss["g_rgb"], loss["g_rgb0"])
-        la.g_rgb, la.g_rgb0 = loss["g_rgb"].data_ptr(), loss["g_rgb0"].data_ptr()
-        a.loss = C.pointer(la)
-        keep_loss = (la, tgt, tv)
     nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
     wsb = _ws(nbytes, dev)
     t0 = TIMER.begin("render_fwd")
@@ -291,7 +268,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
 
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
-               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False):
+               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False, loss=None):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -309,7 +286,13 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     (bitwise the same update, fewer optimizer-state bytes).
     owner_defer=True (binned scatter): the table gradient is not formed yet;
     render_bwd_owner(st, lo, hi) then writes bins [lo, hi) (render_bins
-    gives their geometry), e.g. each range before its gradient exchange."""
+    gives their geometry), e.g. each range before its gradient exchange.
+    loss (ABI 13, the trainer's step): dict(target [B, 3], out [4] device,
+    rgb / rgb0 / sparsity / sparsity0 = the forward's outputs, tv [L] or
+    None, world, sparse_w, tv_w) forms the training loss's upstream
+    gradients in the backward itself (run_nerf.py:612-636 under
+    train.dp_loss's rule; grads is not read) and writes out = loss, mse,
+    mse0, entropy sum (loss_fwd's)."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -363,6 +346,18 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
         keep.append(g_tv)
         a.g_tv = g_tv.data_ptr()
     a.owner_defer = 1 if owner_defer else 0
+    if loss is not None:
+        la = L.HnRenderLoss()
+        ts = [L.contig(loss[k]) for k in ("target", "rgb", "rgb0", "sparsity", "sparsity0")]
+        ltv = loss.get("tv")
+        ltv = L.contig(ltv) if ltv is not None else None
+        L.require_device(*ts, ltv, loss["out"])
+        la.target, la.rgb, la.rgb0, la.sparsity, la.sparsity0 = (t.data_ptr() for t in ts)
+        la.tv, la.n_tv = (ltv.data_ptr(), ltv.numel()) if ltv is not None else (None, 0)
+        la.world, la.sparse_w, la.tv_w = float(loss["world"]), float(loss["sparse_w"]), float(loss["tv_w"])
+        la.out = loss["out"].data_ptr()
+        a.loss = C.pointer(la)
+        keep += ts + [ltv, la]
     t0 = TIMER.begin("render_bwd")
     L.check(L.lib().hn_render_bwd(st.cfg, a, L.ptr(st.wsb), st.nbytes, L.stream(dev)), "render_bwd")
     TIMER.end("render_bwd", t0)

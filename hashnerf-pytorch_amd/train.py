@@ -577,9 +577,9 @@ class Trainer:
         # unless asked for (bench.py --prefetch).
         self.prefetch = False
         self._pf = None          # (step, batch, ready event) drawn ahead
-        # explicit mode: the loss value and its rgb gradients fused into the
-        # render forward (ABI 13; batches of a multiple of 4 rays) instead of
-        # an hn_loss_fwd_bwd launch
+        # explicit mode: the loss value and its gradients formed by the render
+        # backward's composite pre-pass (ABI 13) instead of an hn_loss_fwd_bwd
+        # launch
         self.fuse_loss = True
         self._side = None
 
@@ -722,8 +722,7 @@ class Trainer:
         self._binned = HF.L.lib().hn_render_scatter_mode(self._cfg, a.N_rand) == 2
         self._gws = HF.zeros_like_all(self._ws)
         self._one = torch.ones((), device=self.device)
-        self._lcount = torch.zeros(1, dtype=torch.int32, device=self.device)   # the fused loss's ticket word
-        self._gsp = None
+        self._gtv = None
         self._grads = True
 
     def draw_batch(self, i: Optional[int] = None):
@@ -796,31 +795,26 @@ class Trainer:
             cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
-        # the loss fused into the forward (ABI 13): its gradient w.r.t. rgb /
-        # rgb0 written by the forward's waves, the value reduced by its last
-        # workgroup -- no hn_loss_fwd_bwd launch
-        B = rays.shape[0]
-        fused_loss = self.fuse_loss and B % 4 == 0
-        if fused_loss:
+        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
+        if pf:
+            self._prefetch(i + 1)
+        loss = None
+        if self.fuse_loss:
+            # the loss formed by the backward's composite pre-pass (ABI 13):
+            # its rgb / entropy gradients computed where they are used, its
+            # value by one workgroup -- no hn_loss_fwd_bwd launch
             lo = torch.empty(4, dtype=torch.float32, device=self.device)
-            g_rgb = torch.empty((B, 3), dtype=torch.float32, device=self.device)
-            g_rgb0 = torch.empty((B, 3), dtype=torch.float32, device=self.device)
-            out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True,
-                                    loss=dict(target=target, tv=tv, world=self.world,
-                                              sparse_w=a.sparse_loss_weight, tv_w=a.tv_loss_weight, out=lo,
-                                              counter=self._lcount, g_rgb=g_rgb, g_rgb0=g_rgb0))
-            if pf:
-                self._prefetch(i + 1)
-            # d loss / d entropy = g * sparse_w, d loss / d tv_l = g * tv_w with
-            # g = 1 (hn_loss_bwd's): constants
-            if self._gsp is None or self._gsp.shape[0] != B:
-                self._gsp = torch.full((B,), a.sparse_loss_weight, dtype=torch.float32, device=self.device)
-            grads = dict(g_rgb=g_rgb, g_sparsity=self._gsp, g_rgb0=g_rgb0, g_sparsity0=self._gsp)
-            g_tv = None if tv is None else torch.full_like(tv, a.tv_loss_weight)
+            loss = dict(target=target, rgb=out["rgb"], rgb0=out["rgb0"], sparsity=out["sparsity"],
+                        sparsity0=out["sparsity0"], tv=tv, world=self.world, sparse_w=a.sparse_loss_weight,
+                        tv_w=a.tv_loss_weight, out=lo)
+            grads = {}
+            # d loss / d tv_l = g * tv_w (g = 1, hn_loss_bwd's): a constant vector
+            g_tv = None
+            if tv is not None:
+                if self._gtv is None or self._gtv.shape != tv.shape:
+                    self._gtv = torch.full_like(tv, a.tv_loss_weight)
+                g_tv = self._gtv
         else:
-            out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
-            if pf:
-                self._prefetch(i + 1)
             # loss value and its input gradients in one launch (the gradients do
             # not depend on the value)
             lo, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(
@@ -837,7 +831,7 @@ class Trainer:
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask())
+                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), loss=loss)
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
@@ -845,7 +839,7 @@ class Trainer:
             # DP exchange its owner pass runs per segment inside the exchange
             defer = self._xchg is not None and self._xchg.seg_bins is not None
             HF.render_bwd(st, grads, self._gtable, self._gws, overwrite=True, overwrite_mlp=True, tv=tvb,
-                          owner_defer=defer)
+                          owner_defer=defer, loss=loss)
             self._owner_st = st if defer else None
             table.grad = self._gtable
         for p, g in zip(self._ws, self._gws):

@@ -158,25 +158,25 @@ typedef struct hn_render_cfg {
 #define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the
                                          MLPs' ReLU masks of those points (ABI 10) */
 
-/* ABI 13: the training loss fused into hn_render_fwd (the trainer's step;
+/* ABI 13: the training loss fused into hn_render_bwd (the trainer's step;
  * replaces its hn_loss_fwd_bwd launch).  The loss is run_nerf.py:612-636
  * under train.dp_loss's data-parallel rule:
  *   loss = (mse(rgb) + mse(rgb0)) / world + sparse_w * sum(entropy + entropy0)
  *          + tv_w * sum(tv)
- * With `loss` set the forward also writes its gradient w.r.t. both passes'
- * rgb (hn_loss_bwd's op forms, g_loss = 1; the entropy and TV gradients are
- * the constants sparse_w and tv_w) and reduces the loss value into out[4] =
- * loss, mse, mse0, sum of entropies (hn_loss_fwd's fp64 sums, in another
- * order).  n_rays a multiple of 4. */
+ * With hn_render_bwd_args.loss set, the backward's composite pre-pass forms
+ * the upstream gradients itself from the forward's outputs (hn_loss_bwd's op
+ * forms with g_loss = 1; the g_* arguments are not read) and one of its
+ * workgroups reduces the loss value into out[4] = loss, mse, mse0, sum of
+ * entropies (hn_loss_fwd's fp64 sums, another thread count).  The TV term's
+ * gradient still comes in as tv / g_tv (= tv_w per level). */
 typedef struct hn_render_loss {
   const float* target;      /* [B][3] */
+  const float* rgb; const float* rgb0;            /* the forward's [B][3] outputs */
+  const float* sparsity; const float* sparsity0;  /* the forward's [B] entropies */
   const float* tv;          /* [n_tv] per-level TV values (hn_tv_fwd), or NULL */
   int32_t n_tv;
   float world, sparse_w, tv_w;
   float* out;               /* [4] */
-  uint32_t* counter;        /* device word, 0 on entry and left 0: the last workgroup's ticket */
-  float* g_rgb;             /* [B][3] d loss / d rgb (hn_render_bwd's g_rgb) */
-  float* g_rgb0;            /* [B][3] d loss / d rgb0 */
 } hn_render_loss;
 
 typedef struct hn_render_fwd_args {
@@ -203,7 +203,6 @@ typedef struct hn_render_fwd_args {
   float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
                                evaluated points and their ReLU masks (MFMA-tile order,
                                opaque); NULL = not kept (inference); required by hn_render_bwd */
-  const hn_render_loss* loss;   /* ABI 13: NULL, or the fused training loss (above) */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -258,6 +257,7 @@ typedef struct hn_render_bwd_args {
    * start each range's gradient exchange while the next range is reduced).
    * The workspace must not be touched in between. */
   int32_t owner_defer;
+  const hn_render_loss* loss;   /* ABI 13: NULL, or the training loss formed here (above) */
 } hn_render_bwd_args;
 
 /* The binned scatter's bins for this cfg and batch: returns their number (0:

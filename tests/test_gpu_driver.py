@@ -261,13 +261,13 @@ def test_trainer_prefetch_same_trajectory(hn, batching):
 
 
 @pytest.mark.parametrize("world,tv", [(1, True), (2, False)])
-def test_fused_loss_forward_matches_separate(hn, world, tv):
-    """ABI 13: render_fwd(loss=...) writes the loss's rgb / rgb0 gradients
-    and reduces its value inside the forward.  Against render_fwd +
-    hn_loss_fwd_bwd on the same inputs (4096 rays, T=19): the forward outputs
-    and the gradients are bitwise equal (the same op forms), the loss value
-    agrees to 1e-6 (fp64 sums in another order); the ticket word is left 0.
-    world=2 applies the DP rule."""
+def test_fused_loss_backward_matches_separate(hn, world, tv):
+    """ABI 13: render_bwd(loss=...) forms the loss's gradients in its
+    composite pre-pass and reduces the loss value there.  Against
+    hn_loss_fwd_bwd + render_bwd(grads) on the same forward (4096 rays,
+    T=19): the table and MLP gradients are bitwise equal (the same op forms),
+    the loss value agrees to 1e-6 (fp64 sums, another thread count).  world=2
+    applies the DP rule."""
     from hashnerf_pytorch_amd import functional as HF
     from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
     data = SyntheticBlender(200, 200, 4, DEV, seed=0, scene="procedural")
@@ -278,31 +278,36 @@ def test_fused_loss_forward_matches_separate(hn, world, tv):
     torch.manual_seed(3)
     b = tr.draw_batch(600)
     table = tr.embed_fn.table
-    tvv = None
+    tvv = tvb = None
     if b["tv"] is not None:
         cubes, mv0 = b["tv"]
-        tvv, _ = HF.tv_fwd(table, mv0, cubes, tr.embed_fn.log2_hashmap_size)
+        tvv, mv = HF.tv_fwd(table, mv0, cubes, tr.embed_fn.log2_hashmap_size)
+        tvb = (mv, cubes, torch.full_like(tvv, args.tv_loss_weight))
     consts = (world, args.sparse_loss_weight, args.tv_loss_weight)
-    out_a, _ = HF.render_fwd(tr._cfg, b["rays"], tr._t_vals, b["t_rand"], b["u"], None, None, table, tr._ws, True)
-    lo_a, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(out_a["rgb"], out_a["rgb0"], b["target"],
-                                                               out_a["sparsity"], out_a["sparsity0"], tvv, *consts,
+    out, st = HF.render_fwd(tr._cfg, b["rays"], tr._t_vals, b["t_rand"], b["u"], None, None, table, tr._ws, True)
+    lo_a, (g_rgb, g_rgb0, g_sp, g_sp0, g_tv) = HF.loss_fwd_bwd(out["rgb"], out["rgb0"], b["target"],
+                                                               out["sparsity"], out["sparsity0"], tvv, *consts,
                                                                torch.ones((), device=DEV))
-    lo_b = torch.empty(4, device=DEV)
-    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
-    gb, gb0 = torch.empty_like(g_rgb), torch.empty_like(g_rgb0)
-    out_b, _ = HF.render_fwd(tr._cfg, b["rays"], tr._t_vals, b["t_rand"], b["u"], None, None, table, tr._ws,
-                             True, loss=dict(target=b["target"], tv=tvv, world=world,
-                                             sparse_w=args.sparse_loss_weight, tv_w=args.tv_loss_weight,
-                                             out=lo_b, counter=cnt, g_rgb=gb, g_rgb0=gb0))
-    torch.cuda.synchronize()
-    for k in ("rgb", "rgb0", "depth", "acc", "sparsity", "sparsity0", "z_fine", "raw_f"):
-        assert torch.equal(out_a[k], out_b[k]), k
-    assert torch.equal(g_rgb, gb) and torch.equal(g_rgb0, gb0)
-    assert torch.equal(g_sp, torch.full_like(g_sp, args.sparse_loss_weight))
     if tvv is not None:
-        assert torch.equal(g_tv, torch.full_like(tvv, args.tv_loss_weight))
-    assert int(cnt.item()) == 0, "the ticket word must be left 0 for the next launch"
-    torch.testing.assert_close(lo_b, lo_a, rtol=1e-6, atol=0)
+        assert torch.equal(g_tv, tvb[2])
+    res = []
+    for fused in (False, True):
+        d_table = torch.empty_like(table)
+        dws = HF.zeros_like_all(tr._ws)
+        lo_b = torch.empty(4, device=DEV)
+        grads = dict(g_rgb=g_rgb, g_sparsity=g_sp, g_rgb0=g_rgb0, g_sparsity0=g_sp0)
+        loss = None if not fused else dict(
+            target=b["target"], rgb=out["rgb"], rgb0=out["rgb0"], sparsity=out["sparsity"],
+            sparsity0=out["sparsity0"], tv=tvv, world=world, sparse_w=args.sparse_loss_weight,
+            tv_w=args.tv_loss_weight, out=lo_b)
+        HF.render_bwd(st, {} if fused else grads, d_table, dws, overwrite=True, overwrite_mlp=True, tv=tvb,
+                      loss=loss)
+        torch.cuda.synchronize()
+        res.append((d_table, dws, lo_b))
+    assert torch.equal(res[0][0], res[1][0])
+    for x, y in zip(res[0][1], res[1][1]):
+        assert torch.equal(x, y)
+    torch.testing.assert_close(res[1][2], lo_a, rtol=1e-6, atol=0)
 
 
 def test_trainer_fused_loss_same_trajectory(hn):
