@@ -376,32 +376,33 @@ HN_DEV void mlp_bwd_tile(const float* __restrict__ P, const f32x16& feat, const 
 }
 
 // Packing: natural torch weights -> fragment-ordered A operands (per net).
-// f32 value of region r's A fragment: out block ob, k-step s, lane.
-HN_DEV float pack_f32(const hn_mlp& w, int r, int ob, int s, int lane) {
+// f32 value of region r's A fragment: out block ob, k-step s, lane; W(t, i) =
+// element i of torch tensor t (0 sigma_net.0 .. 4 color_net.2).
+template <class W>
+HN_DEV float pack_f32(const W& w, int r, int ob, int s, int lane) {
   const int i = lane & 31, h = lane >> 5;
   const int o = ob * 32 + i;
   const int kc = 32 * (s >> 4) + row_of(s & 15, h);   // chain order (D-layout input)
   const int kp = 2 * s + h;                            // pair order
   switch (r) {
-    case R_F0: return w.sigma0[o * 32 + kc];
-    case R_F1: return i < 16 ? w.sigma1[i * 64 + kc] : 0.f;
-    case R_F2G: return (kc >= 1 && kc <= 15) ? w.color0[o * 31 + 15 + kc] : 0.f;
-    case R_F2S: return w.color0[o * 31 + kp];
-    case R_F3: return w.color1[o * 64 + kc];
-    case R_F4: return i < 3 ? w.color2[i * 64 + kc] : 0.f;
-    case R_B4: return kp < 3 ? w.color2[kp * 64 + o] : 0.f;
-    case R_B3: return w.color1[kc * 64 + o];
-    case R_B2G: return (i >= 1 && i <= 15) ? w.color0[kc * 31 + 15 + i] : 0.f;
-    case R_B2S: return i < 16 ? w.color0[kc * 31 + i] : 0.f;
-    case R_B1: return w.sigma1[kc * 64 + o];
-    default: return w.sigma0[kc * 32 + i];   // R_B0
+    case R_F0: return w(0, o * 32 + kc);
+    case R_F1: return i < 16 ? w(1, i * 64 + kc) : 0.f;
+    case R_F2G: return (kc >= 1 && kc <= 15) ? w(2, o * 31 + 15 + kc) : 0.f;
+    case R_F2S: return w(2, o * 31 + kp);
+    case R_F3: return w(3, o * 64 + kc);
+    case R_F4: return i < 3 ? w(4, i * 64 + kc) : 0.f;
+    case R_B4: return kp < 3 ? w(4, kp * 64 + o) : 0.f;
+    case R_B3: return w(3, kc * 64 + o);
+    case R_B2G: return (i >= 1 && i <= 15) ? w(2, kc * 31 + 15 + i) : 0.f;
+    case R_B2S: return i < 16 ? w(2, kc * 31 + i) : 0.f;
+    case R_B1: return w(1, kc * 64 + o);
+    default: return w(0, kc * 32 + i);   // R_B0
   }
 }
 
-// Float idx of the packed buffer (layout above).
-HN_DEV float pack_value(const hn_mlp& w, int idx) {
-  int r = 0;
-  while (r + 1 < R_N && idx >= reg_off(r + 1)) ++r;
+// Float idx of the packed buffer (layout above), inside region r.
+template <class W>
+HN_DEV float pack_value_r(const W& w, int r, int idx) {
   const int rel = idx - reg_off(r), d = rel & 3, lane = (rel >> 2) & 63, t = rel >> 8;
   const int gpo = reg_gpo(r), ns = reg_ns(r), g = t % gpo, ob = t / gpo;
   if (ns == 0) return pack_f32(w, r, ob, 4 * g + d, lane);
@@ -418,6 +419,24 @@ HN_DEV float pack_value(const hn_mlp& w, int idx) {
     out |= (uint32_t)__builtin_bit_cast(uint16_t, b) << (16 * e);
   }
   return __uint_as_float(out);
+}
+// the natural weights of one net (hn_mlp's tensors)
+struct MlpW {
+  const hn_mlp& m;
+  HN_DEV float operator()(int t, int i) const {
+    const float* p = t == 0 ? m.sigma0 : t == 1 ? m.sigma1 : t == 2 ? m.color0 : t == 3 ? m.color1 : m.color2;
+    return p[i];
+  }
+};
+HN_DEV float pack_value(const hn_mlp& w, int idx) {
+  int r = 0;
+  while (r + 1 < R_N && idx >= reg_off(r + 1)) ++r;
+  return pack_value_r(MlpW{w}, r, idx);
+}
+// the torch tensor (0 sigma_net.0 .. 4 color_net.2) a region's values come from
+constexpr int reg_layer(int r) {
+  return r == R_F0 || r == R_B0 ? 0 : r == R_F1 || r == R_B1 ? 1 : r == R_F3 || r == R_B3 ? 3
+         : r == R_F4 || r == R_B4 ? 4 : 2;
 }
 
 // Launch the packing kernel (hn_mlp.hip).

@@ -2371,11 +2371,14 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (k.bins && blockIdx.x == 0) zero_ovf_book(k);   // binned scatter: no overflow records yet
-  // the loss value (hn_loss_fwd's reduction) by workgroup 0, beside its rays
-  if (k.lout && blockIdx.x == 0)
+  // the loss value (hn_loss_fwd's reduction): an extra workgroup 0 of its own,
+  // dispatched first, so its serial sums run beside the rays' workgroups
+  if (k.lout && blockIdx.x == 0) {
     loss_fwd_block<64 * kFwdWaves>(k.lrgb, k.lrgb0, k.ltarget, k.lsp, k.lsp0, k.B, k.ltv, k.n_tv, k.lworld,
                                    k.lsparse_w, k.ltv_w, k.lout);
-  const int64_t w = (int64_t)blockIdx.x * kFwdWaves + wave;
+    return;
+  }
+  const int64_t w = (int64_t)(blockIdx.x - (k.lout ? 1 : 0)) * kFwdWaves + wave;
   if (w >= 2 * k.B) return;
   const int64_t ray = w >> 1;
   const bool fine = (w & 1) != 0;
@@ -3073,7 +3076,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   hipStream_t s = (hipStream_t)stream;
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
-  if ((st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
+  if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   RenderK k;
   k.g = make_grid_args(cfg->grid);
   k.white = cfg->white_bkgd;
@@ -3257,7 +3260,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     const size_t tb = ((size_t)16 << T) * 2 * sizeof(float);
     if ((st = hip_status(hipMemsetAsync(a->d_table, 0, tb, s)))) return st;
   }
-  hipLaunchKernelGGL(render_comp_bwd_kernel, dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves)),
+  hipLaunchKernelGGL(render_comp_bwd_kernel,
+                     dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves + (k.lout ? 1 : 0))),
                      dim3(64 * kFwdWaves), 0, s, k);
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL

@@ -221,9 +221,12 @@ class RenderState:
                  "fine_src", "feat", "wsb", "nbytes", "bwd_args")
 
 
-def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat):
+def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None,
+               weights_packed=False):
     """hn_render_fwd (run_nerf_helpers.py:464-574, forward).  Returns the
-    output dict and a RenderState (None when keep_feat is False)."""
+    output dict and a RenderState (None when keep_feat is False).  wsb: the
+    caller's workspace (uint8, >= workspace_bytes; default a fresh one);
+    weights_packed: it already holds ws's packed copies (radam_pack)."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -251,7 +254,13 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
                        device=dev)
     a.feat = feat.data_ptr() if keep_feat else None
     nbytes = L.lib().hn_render_workspace_bytes(cfg, B)
-    wsb = _ws(nbytes, dev)
+    if wsb is None:
+        wsb = _ws(nbytes, dev)
+    elif wsb.numel() * wsb.element_size() < nbytes or not wsb.is_contiguous() or wsb.device != dev:
+        raise ValueError(f"hashnerf_amd.render_fwd: wsb must be a contiguous buffer of >= {nbytes} bytes on {dev}")
+    else:
+        nbytes = wsb.numel() * wsb.element_size()
+    a.weights_packed = 1 if weights_packed else 0
     t0 = TIMER.begin("render_fwd")
     L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
     TIMER.end("render_fwd", t0)
@@ -653,23 +662,42 @@ class TVFn(torch.autograd.Function):
         return dtable, None, None, None
 
 
+def _radam_array(tensors, name):
+    arr = (L.HnRadamTensor * len(tensors))()
+    for d, (p, g, m, v, c) in zip(arr, tensors):
+        L.require_device(p, g, m, v)
+        for t in (p, g, m, v):
+            if not t.is_contiguous():
+                raise RuntimeError(f"hashnerf_amd.{name}: tensors must be contiguous")
+        d.p, d.g, d.m, d.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+        d.n = p.numel()
+        for k in ("beta1", "beta2", "one_minus_beta1", "one_minus_beta2", "eps", "neg_wd_lr",
+                  "neg_step_lr", "mode", "has_wd"):
+            setattr(d, k, c[k])
+    return arr
+
+
 def radam_step(tensors):
     """tensors: list of (p, g, m, v, coeff dict); one HIP launch per 16 tensors."""
     for i in range(0, len(tensors), L.RADAM_MAX_TENSORS):
         chunk = tensors[i:i + L.RADAM_MAX_TENSORS]
-        arr = (L.HnRadamTensor * len(chunk))()
-        dev = chunk[0][0].device
-        for d, (p, g, m, v, c) in zip(arr, chunk):
-            L.require_device(p, g, m, v)
-            for t in (p, g, m, v):
-                if not t.is_contiguous():
-                    raise RuntimeError("hashnerf_amd.radam_step: tensors must be contiguous")
-            d.p, d.g, d.m, d.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
-            d.n = p.numel()
-            for k in ("beta1", "beta2", "one_minus_beta1", "one_minus_beta2", "eps", "neg_wd_lr",
-                      "neg_step_lr", "mode", "has_wd"):
-                setattr(d, k, c[k])
-        L.check(L.lib().hn_radam_step(arr, len(chunk), L.stream(dev)), "radam_step")
+        arr = _radam_array(chunk, "radam_step")
+        L.check(L.lib().hn_radam_step(arr, len(chunk), L.stream(chunk[0][0].device)), "radam_step")
+
+
+def radam_pack(tensors, wsb):
+    """hn_render_radam_pack: the RAdam step of the ten NeRFSmall tensors
+    (tensors = [(p, g, m, v, coeffs)] in render_fwd's ws order: network_fn's
+    five, then network_fine's) fused with their MFMA packing into the render
+    workspace wsb; the next render_fwd(wsb=wsb, weights_packed=True) then
+    skips its packing."""
+    if len(tensors) != 10:
+        raise ValueError("hashnerf_amd.radam_pack: the ten NeRFSmall tensors (coarse 5, fine 5)")
+    if not wsb.is_cuda or not wsb.is_contiguous():
+        raise RuntimeError("hashnerf_amd.radam_pack: wsb must be a contiguous device buffer")
+    arr = _radam_array(tensors, "radam_pack")
+    L.check(L.lib().hn_render_radam_pack(arr, L.ptr(wsb), wsb.numel() * wsb.element_size(),
+                                         L.stream(wsb.device)), "radam_pack")
 
 
 SCATTER_MODES = {"auto": 0, "atomic": 1, "binned": 2}
