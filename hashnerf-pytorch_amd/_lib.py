@@ -60,7 +60,7 @@ class HnRenderFwdArgs(C.Structure):
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
                 ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
-                ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32)]
+                ("fine_src", _P), ("feat", _P)]
 
 
 class HnRadamTensor(C.Structure):
@@ -124,7 +124,6 @@ SIGNATURES = {
     "hn_tv_fwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P]),
     "hn_tv_bwd": (C.c_int32, [C.POINTER(HnTvArgs), _P, _P, _P]),
     "hn_radam_step": (C.c_int32, [C.POINTER(HnRadamTensor), C.c_int32, _P]),
-    "hn_render_radam_pack": (C.c_int32, [C.POINTER(HnRadamTensor), _P, C.c_size_t, _P]),
     "hn_sample_rays": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P]),
     "hn_sample_rays_morton_workspace_bytes": (C.c_size_t, [C.POINTER(HnRaySampler)]),
     "hn_sample_rays_morton": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P, C.c_size_t,

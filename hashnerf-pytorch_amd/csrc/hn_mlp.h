@@ -433,11 +433,6 @@ HN_DEV float pack_value(const hn_mlp& w, int idx) {
   while (r + 1 < R_N && idx >= reg_off(r + 1)) ++r;
   return pack_value_r(MlpW{w}, r, idx);
 }
-// the torch tensor (0 sigma_net.0 .. 4 color_net.2) a region's values come from
-constexpr int reg_layer(int r) {
-  return r == R_F0 || r == R_B0 ? 0 : r == R_F1 || r == R_B1 ? 1 : r == R_F3 || r == R_B3 ? 3
-         : r == R_F4 || r == R_B4 ? 4 : 2;
-}
 
 // Launch the packing kernel (hn_mlp.hip).
 int32_t mlp_pack_launch(const hn_mlp* w, float* packed, hipStream_t s);

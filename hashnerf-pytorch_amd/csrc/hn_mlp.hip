@@ -125,61 +125,6 @@ __global__ __launch_bounds__(256) void mlp_pack2_kernel(hn_mlp w0, float* __rest
   }
 }
 
-// RAdam of the ten NeRFSmall tensors fused with their packing: workgroup
-// (net, layer) steps that tensor (radam_kernel's per-element update), keeps
-// the new weights in LDS and writes the regions packed from them (pack_value's
-// values), so no other workgroup reads a weight it may be writing.
-constexpr int kRpLayerMax = 64 * 64;   // color_net.1, the largest tensor
-constexpr int kRpNumel[5] = {64 * 32, 16 * 64, 64 * 31, 64 * 64, 3 * 64};
-// the regions of one tensor, each with compile-time geometry (its divisions
-// and the value switch fold away)
-template <int R, class W>
-HN_DEV void rp_regions(const W& w, int layer, float* __restrict__ P) {
-  if constexpr (R < R_N) {
-    if (reg_layer(R) == layer)
-      for (int idx = reg_off(R) + (int)threadIdx.x; idx < reg_off(R + 1); idx += 1024)
-        P[idx] = pack_value_r(w, R, idx);
-    rp_regions<R + 1>(w, layer, P);
-  }
-}
-struct RadamPackK {
-  hn_radam_tensor t[10];
-  float* P;   // [2][G_END]: network_fn's packed copy, then network_fine's
-};
-__global__ __launch_bounds__(1024) void radam_pack_kernel(RadamPackK k) {
-  __shared__ float w[kRpLayerMax + kRpLayerMax / 32];   // element i at i + i / 32 (rows of 64 / 32: no bank conflicts)
-  const int net = blockIdx.x / 5, layer = blockIdx.x % 5;
-  const hn_radam_tensor& d = k.t[blockIdx.x];
-  const int n = (int)d.n;
-  // every load of the thread's (<= 4) elements in flight at once: one round trip
-  constexpr int kPer = kRpLayerMax / 1024;
-  float p[kPer], g[kPer], m[kPer], v[kPer];
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int i = threadIdx.x + j * 1024;
-    if (i < n) {
-      p[j] = d.p[i]; g[j] = d.g[i]; m[j] = d.m[i]; v[j] = d.v[i];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int i = threadIdx.x + j * 1024;
-    if (i < n) {
-      radam_elem(d, p[j], g[j], m[j], v[j]);
-      d.m[i] = m[j];
-      d.v[i] = v[j];
-      if (d.mode != 0) d.p[i] = p[j];
-      w[i + (i >> 5)] = p[j];
-    }
-  }
-  __syncthreads();
-  // the weights read straight from the LDS array (ds_read: a generic pointer
-  // would make each read wait for the previous packed stores, vmcnt)
-  auto lw = [&](int, int i) { return w[i + (i >> 5)]; };
-  float* P = k.P + (size_t)net * G_END;
-  rp_regions<0>(lw, layer, P);
-}
-
 int32_t hn::mlp_pack2_launch(const hn_mlp* w0, float* p0, const hn_mlp* w1, float* p1, hipStream_t s) {
   hipLaunchKernelGGL(mlp_pack2_kernel, dim3((G_END + 255) / 256, 2), dim3(256), 0, s, *w0, p0, *w1, p1);
   return hip_status(hipGetLastError());
@@ -225,20 +170,5 @@ extern "C" int32_t hn_mlp_bwd(const hn_mlp* w, const float* x, const float* dout
   if (blocks > 512) blocks = 512;
   const size_t lds = (size_t)(W_END + kBwdWaves * 2 * kTBuf) * sizeof(float);
   hipLaunchKernelGGL(mlp_bwd_kernel, dim3((unsigned)blocks), dim3(256), lds, s, P, x, dout, n, dx, *dw);
-  return hip_status(hipGetLastError());
-}
-
-extern "C" int32_t hn_render_radam_pack(const hn_radam_tensor* ts, void* workspace, size_t ws_bytes,
-                                        void* stream) {
-  if (!ts || !workspace) return HN_E_NULL;
-  if (ws_bytes < (size_t)2 * G_END * sizeof(float)) return HN_E_WORKSPACE;
-  RadamPackK k;
-  for (int i = 0; i < 10; ++i) {
-    if (!ts[i].p || !ts[i].g || !ts[i].m || !ts[i].v) return HN_E_NULL;
-    if (ts[i].n != kRpNumel[i % 5]) return HN_E_SHAPE;
-    k.t[i] = ts[i];
-  }
-  k.P = (float*)workspace;
-  hipLaunchKernelGGL(radam_pack_kernel, dim3(10), dim3(1024), 0, (hipStream_t)stream, k);
   return hip_status(hipGetLastError());
 }

@@ -3076,7 +3076,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   hipStream_t s = (hipStream_t)stream;
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
-  if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
+  if ((st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   RenderK k;
   k.g = make_grid_args(cfg->grid);
   k.white = cfg->white_bkgd;

@@ -221,12 +221,10 @@ class RenderState:
                  "fine_src", "feat", "wsb", "nbytes", "bwd_args")
 
 
-def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None,
-               weights_packed=False):
+def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None):
     """hn_render_fwd (run_nerf_helpers.py:464-574, forward).  Returns the
     output dict and a RenderState (None when keep_feat is False).  wsb: the
-    caller's workspace (uint8, >= workspace_bytes; default a fresh one);
-    weights_packed: it already holds ws's packed copies (radam_pack)."""
+    caller's workspace (uint8, >= workspace_bytes; default a fresh one)."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -260,7 +258,6 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
         raise ValueError(f"hashnerf_amd.render_fwd: wsb must be a contiguous buffer of >= {nbytes} bytes on {dev}")
     else:
         nbytes = wsb.numel() * wsb.element_size()
-    a.weights_packed = 1 if weights_packed else 0
     t0 = TIMER.begin("render_fwd")
     L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
     TIMER.end("render_fwd", t0)
@@ -683,21 +680,6 @@ def radam_step(tensors):
         chunk = tensors[i:i + L.RADAM_MAX_TENSORS]
         arr = _radam_array(chunk, "radam_step")
         L.check(L.lib().hn_radam_step(arr, len(chunk), L.stream(chunk[0][0].device)), "radam_step")
-
-
-def radam_pack(tensors, wsb):
-    """hn_render_radam_pack: the RAdam step of the ten NeRFSmall tensors
-    (tensors = [(p, g, m, v, coeffs)] in render_fwd's ws order: network_fn's
-    five, then network_fine's) fused with their MFMA packing into the render
-    workspace wsb; the next render_fwd(wsb=wsb, weights_packed=True) then
-    skips its packing."""
-    if len(tensors) != 10:
-        raise ValueError("hashnerf_amd.radam_pack: the ten NeRFSmall tensors (coarse 5, fine 5)")
-    if not wsb.is_cuda or not wsb.is_contiguous():
-        raise RuntimeError("hashnerf_amd.radam_pack: wsb must be a contiguous device buffer")
-    arr = _radam_array(tensors, "radam_pack")
-    L.check(L.lib().hn_render_radam_pack(arr, L.ptr(wsb), wsb.numel() * wsb.element_size(),
-                                         L.stream(wsb.device)), "radam_pack")
 
 
 SCATTER_MODES = {"auto": 0, "atomic": 1, "binned": 2}

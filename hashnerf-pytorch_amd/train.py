@@ -576,12 +576,6 @@ class Trainer:
         # cross-stream waits cost more than the launches they move), so off
         # unless asked for (bench.py --prefetch).
         self.prefetch = False
-        # explicit mode: the MLP tensors' RAdam step fused with their MFMA
-        # packing into the render workspace (hn_render_radam_pack), which the
-        # next forward then reuses instead of repacking
-        self.fuse_mlp_step = True
-        self._rws = None         # the render workspace, kept across steps
-        self._pk = None          # (workspace, weight versions) the packed copies belong to
         self._pf = None          # (step, batch, ready event) drawn ahead
         # explicit mode: the loss value and its gradients formed by the render
         # backward's composite pre-pass (ABI 13) instead of an hn_loss_fwd_bwd
@@ -801,11 +795,7 @@ class Trainer:
             cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
-        nb = HF.L.lib().hn_render_workspace_bytes(self._cfg, rays.shape[0])
-        if self._rws is None or self._rws.numel() < nb:
-            self._rws, self._pk = torch.empty(nb, dtype=torch.uint8, device=self.device), None
-        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True,
-                                wsb=self._rws, weights_packed=self._pk == self._pack_key())
+        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
         if pf:
             self._prefetch(i + 1)
         loss = None
@@ -855,28 +845,6 @@ class Trainer:
         for p, g in zip(self._ws, self._gws):
             p.grad = g
         return lo[0], lo[1]
-
-    def _pack_key(self):
-        """What the workspace's packed weights must match: the buffer and
-        every weight's version counter (an in-place change, e.g. a
-        checkpoint load, bumps it; the HIP optimizer writes do not)."""
-        return (self._rws.data_ptr(), tuple(p._version for p in self._ws))
-
-    def _mlp_step_packed(self) -> bool:
-        """The ten MLP tensors' RAdam step fused with their packing into the
-        render workspace (explicit mode); False when it does not apply and
-        optimizer.step() takes them."""
-        if not (self.fuse_mlp_step and self.mode == "explicit" and self._rws is not None and
-                self.device.type == "cuda" and all(p.grad is not None for p in self._ws)):
-            self._pk = None
-            return False
-        ts = []
-        for p in self._ws:
-            _, m, v, c = self.optimizer.take_step(p)
-            ts.append((p, p.grad, m, v, c))
-        HF.radam_pack(ts, self._rws)
-        self._pk = self._pack_key()
-        return True
 
     def _empty_rank_grads(self, batch):
         """A rank that drew no rays this step (world > 1, use_batching: the
@@ -960,7 +928,6 @@ class Trainer:
             table.grad = None
         else:
             self.allreduce_grads()
-        self._mlp_step_packed()
         self.optimizer.step()
         decay_steps = a.lrate_decay * 1000
         new_lr = a.lrate * (0.1 ** (self.global_step / decay_steps))

@@ -203,9 +203,6 @@ typedef struct hn_render_fwd_args {
   float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
                                evaluated points and their ReLU masks (MFMA-tile order,
                                opaque); NULL = not kept (inference); required by hn_render_bwd */
-  int32_t weights_packed;   /* ABI 13: nonzero = `workspace` already holds both nets' packed MFMA
-                               copies of these weights (hn_render_radam_pack wrote them and the
-                               weights are unchanged since): the forward does not repack them */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -307,15 +304,6 @@ typedef struct hn_radam_tensor {
   int32_t reserved;
 } hn_radam_tensor;
 int32_t hn_radam_step(const hn_radam_tensor* ts, int32_t n_tensors, void* stream);
-/* ABI 13: the RAdam step of both NeRFSmall nets (hn_radam_step's per-element
- * update; radam.py:58-92 as the trainer applies it, run_nerf.py:642) fused
- * with their MFMA packing.  ts[0..4] = network_fn's sigma_net.0, sigma_net.1,
- * color_net.0, color_net.1, color_net.2 (hn_mlp order, numel 2048, 1024,
- * 1984, 4096, 192), ts[5..9] = network_fine's.  Afterwards `workspace` (an
- * hn_render workspace) holds the updated weights' packed copies, so the next
- * hn_render_fwd on it may set weights_packed: one launch instead of
- * hn_radam_step over these tensors plus the forward's packing. */
-int32_t hn_render_radam_pack(const hn_radam_tensor* ts, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- L5 training-step driver (run_nerf.py:576-636) -----------------------
  * Device ray sampler: n_rays DISTINCT pixels of one training image drawn

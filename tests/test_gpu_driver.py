@@ -336,80 +336,3 @@ def test_trainer_fused_loss_same_trajectory(hn):
         assert torch.equal(a[k], b[k]), k
     for x, y in zip(a[4], b[4]):
         assert torch.equal(x, y)
-
-
-def test_radam_pack_matches_separate(hn):
-    """hn_render_radam_pack (ABI 13) against hn_radam_step + the forward's own
-    packing: p, m, v bitwise equal (radam_kernel's per-element update) and the
-    workspace's packed copies byte-identical to what render_fwd packs from the
-    stepped weights; every update form (mode 0 / 1 / 2, weight decay)."""
-    from hashnerf_pytorch_amd import functional as HF
-    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
-    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
-    tr = Trainer(default_args(N_rand=256, log2_hashmap_size=14), data, DEV, seed=2)
-    tr._fused_setup()
-    b = tr.draw_batch(600)
-    g = torch.Generator(device="cpu").manual_seed(5)
-    pk = 2 * HF.L.lib().hn_mlp_workspace_bytes()
-    for mode, wd in ((2, 1e-4), (1, 0.0), (0, 0.0)):
-        c = {"beta1": 0.9, "beta2": 0.99, "one_minus_beta1": 1 - 0.9, "one_minus_beta2": 1 - 0.99, "eps": 1e-15,
-             "neg_wd_lr": -wd * 1e-2, "neg_step_lr": -0.37 * 1e-2 if mode else 0.0, "mode": mode,
-             "has_wd": int(wd != 0)}
-        base = [(torch.randn(p.shape, generator=g) * 0.1, torch.randn(p.shape, generator=g) * 1e-3,
-                 torch.randn(p.shape, generator=g) * 1e-3, torch.rand(p.shape, generator=g) * 1e-6)
-                for p in tr._ws]
-        res = []
-        for fused in (False, True):
-            ps = [x[0].to(DEV) for x in base]
-            gs = [x[1].to(DEV) for x in base]
-            ms = [x[2].to(DEV) for x in base]
-            vs = [x[3].to(DEV) for x in base]
-            ts = [(p, gg, m, v, c) for p, gg, m, v in zip(ps, gs, ms, vs)]
-            nb = HF.L.lib().hn_render_workspace_bytes(tr._cfg, b["rays"].shape[0])
-            wsb = torch.zeros(nb, dtype=torch.uint8, device=DEV)
-            if fused:
-                HF.radam_pack(ts, wsb)
-            else:
-                HF.radam_step(ts)
-                HF.render_fwd(tr._cfg, b["rays"], tr._t_vals, b["t_rand"], b["u"], None, None,
-                              tr.embed_fn.table, ps, False, wsb=wsb)
-            torch.cuda.synchronize()
-            res.append((ps, ms, vs, wsb[:pk].clone()))
-        for k in range(3):
-            for x, y in zip(res[0][k], res[1][k]):
-                assert torch.equal(x, y), (mode, k)
-        assert torch.equal(res[0][3], res[1][3]), mode
-
-
-def test_trainer_fused_mlp_step_same_trajectory(hn):
-    """Trainer.fuse_mlp_step (the MLP RAdam step + packing in one launch, the
-    next forward reusing the packed copies) against optimizer.step() + the
-    forward's packing: 8 steps leave every weight, the table and the moments
-    bitwise equal; a weight changed in place between steps (version bump) is
-    repacked."""
-    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
-    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
-    res = {}
-    for fm in (False, True):
-        args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=5,
-                            sparse_loss_weight=1e-3)
-        tr = Trainer(args, data, DEV, seed=3)
-        tr.fuse_mlp_step = fm
-        torch.manual_seed(11)
-        losses = [float(tr.step()[0]) for _ in range(6)]
-        with torch.no_grad():
-            tr._ws[3].mul_(0.5)          # an in-place change: the packed copies are stale
-        losses += [float(tr.step()[0]) for _ in range(2)]
-        t = tr.embed_fn.table
-        st = tr.optimizer.state[t]
-        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
-        res[fm] = (losses, t.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(),
-                   [p.detach().clone() for p in ws],
-                   [tr.optimizer.state[p]["exp_avg_sq"].clone() for p in ws])
-    a, b = res[False], res[True]
-    assert a[0] == b[0]
-    for k in (1, 2, 3):
-        assert torch.equal(a[k], b[k]), k
-    for k in (4, 5):
-        for x, y in zip(a[k], b[k]):
-            assert torch.equal(x, y), k
