@@ -98,6 +98,13 @@ class HnRaySampler(C.Structure):
                 ("seed", C.c_uint64)]
 
 
+class HnUniformDraw(C.Structure):
+    _fields_ = [("out", _P), ("numel", C.c_int64), ("threads", C.c_int64), ("offset", C.c_uint64)]
+
+
+UNIFORM_MAX_DRAWS = 4
+
+
 class HnRayPool(C.Structure):
     _fields_ = [("n_images", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("pose_stride", C.c_int32),
                 ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
@@ -126,6 +133,9 @@ SIGNATURES = {
     "hn_radam_step": (C.c_int32, [C.POINTER(HnRadamTensor), C.c_int32, _P]),
     "hn_sample_rays": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P]),
     "hn_sample_rays_morton_workspace_bytes": (C.c_size_t, [C.POINTER(HnRaySampler)]),
+    "hn_uniform_philox": (C.c_int32, [C.c_uint64, C.POINTER(HnUniformDraw), C.c_int32, _P]),
+    "hn_sample_batch_morton": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P, C.c_size_t,
+                                           C.c_uint64, C.POINTER(HnUniformDraw), C.c_int32, _P]),
     "hn_sample_rays_morton": (C.c_int32, [C.POINTER(HnRaySampler), _P, _P, C.c_int64, _P, _P, _P, C.c_size_t,
                                           _P]),
     "hn_sample_pool": (C.c_int32, [C.POINTER(HnRayPool), _P, _P, _P, C.c_int64, C.c_int64, _P, _P, _P]),

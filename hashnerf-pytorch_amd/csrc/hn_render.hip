@@ -2671,7 +2671,10 @@ HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_
 // ids through LDS cursors (spilled records clump into few bins: per-record
 // global cursors serialise on them).  Returns at once when nothing spilled
 // (the usual case).
-constexpr int kPlaceThreads = 1024;
+#ifndef HN_PLACE_THREADS
+#define HN_PLACE_THREADS 1024
+#endif
+constexpr int kPlaceThreads = HN_PLACE_THREADS;
 __global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
   __shared__ uint32_t cur[kScMaxBins], lc[kScMaxBins];
   __shared__ uint32_t part[kPlaceThreads];

@@ -80,8 +80,56 @@ HN_DEV uint32_t morton_drawn(const hn_ray_sampler& s, int half, int64_t n, uint3
   return (int64_t)y < n ? x : ~0u;
 }
 
+// torch.rand on the CUDA/HIP default generator, restated (ATen's
+// distribution_elementwise_grid_stride_kernel with hiprand's Philox4x32-10,
+// unroll 4): element li of a draw comes from thread idx = li % T of torch's
+// launch (T threads), its call it = li / (4T) and component (li / T) % 4 --
+// Philox of counter (offset / 4 + it, subsequence idx) under key = seed,
+// mapped by rocrand's 2^-32 + v * 2^-32 to (0, 1], and 1 -> 0 (uniform_'s
+// bound reversal).
+struct UniK {
+  uint32_t key[2];
+  int n;
+  int64_t start[HN_UNIFORM_MAX_DRAWS + 1];   // element prefix of the draws
+  hn_uniform_draw d[HN_UNIFORM_MAX_DRAWS];
+};
+HN_DEV uint32_t philox_component(uint64_t ctr, uint64_t sub, uint32_t k0, uint32_t k1, int comp) {
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = (uint32_t)sub, c3 = (uint32_t)(sub >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return comp == 0 ? c0 : comp == 1 ? c1 : comp == 2 ? c2 : c3;
+}
+// global element g of the UniK's draws
+HN_DEV void uniform_elem(const UniK& u, int64_t g) {
+  int j = 0;
+  while (j + 1 < u.n && g >= u.start[j + 1]) ++j;
+  const hn_uniform_draw& d = u.d[j];
+  const int64_t li = g - u.start[j];
+  const uint64_t T = (uint64_t)d.threads, idx = (uint64_t)li % T, rem = (uint64_t)li / T;
+  const uint32_t v = philox_component(d.offset / 4 + (rem >> 2), idx, u.key[0], u.key[1], (int)(rem & 3));
+  const float x = 0x1p-32f + (float)v * 0x1p-32f;
+  d.out[li] = x == 1.f ? 0.f : x;
+}
+__global__ __launch_bounds__(1024) void uniform_kernel(UniK u) {
+  const int64_t g = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (g < u.start[u.n]) uniform_elem(u, g);
+}
+
 __global__ __launch_bounds__(kMortonThreads) void morton_count_kernel(hn_ray_sampler s, int half, int64_t n,
-                                                                      uint32_t n_idx, int* __restrict__ counts) {
+                                                                      uint32_t n_idx, int* __restrict__ counts,
+                                                                      UniK u, unsigned count_blocks) {
+  if (blockIdx.x >= count_blocks) {   // the batch's uniform draws, beside the counts
+    const int64_t g = (int64_t)(blockIdx.x - count_blocks) * kMortonThreads + threadIdx.x;
+    if (g < u.start[u.n]) uniform_elem(u, g);
+    return;
+  }
   const uint32_t m = blockIdx.x * kMortonThreads + threadIdx.x;
   const bool sel = m < n_idx && morton_drawn(s, half, n, m) != ~0u;
   const int c = __syncthreads_count(sel);
@@ -340,9 +388,58 @@ extern "C" size_t hn_sample_rays_morton_workspace_bytes(const hn_ray_sampler* s)
   return (size_t)blocks * sizeof(int);
 }
 
+static int32_t make_uni(uint64_t seed, const hn_uniform_draw* draws, int32_t n_draws, UniK& u) {
+  if (n_draws < 0 || n_draws > HN_UNIFORM_MAX_DRAWS) return HN_E_SHAPE;
+  if (n_draws && !draws) return HN_E_NULL;
+  u.key[0] = (uint32_t)seed;
+  u.key[1] = (uint32_t)(seed >> 32);
+  u.n = n_draws;
+  u.start[0] = 0;
+  for (int j = 0; j < n_draws; ++j) {
+    const hn_uniform_draw& d = draws[j];
+    if (d.numel < 0 || (d.numel && d.threads <= 0) || (d.offset & 3)) return HN_E_SHAPE;
+    if (d.numel && !d.out) return HN_E_NULL;
+    u.d[j] = d;
+    u.start[j + 1] = u.start[j] + d.numel;
+  }
+  return HN_OK;
+}
+
+extern "C" int32_t hn_uniform_philox(uint64_t seed, const hn_uniform_draw* draws, int32_t n_draws, void* stream) {
+  UniK u;
+  const int32_t st = make_uni(seed, draws, n_draws, u);
+  if (st) return st;
+  const int64_t total = u.start[u.n];
+  if (total == 0) return HN_OK;
+  hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)((total + 1023) / 1024)), dim3(1024), 0, (hipStream_t)stream, u);
+  return hip_status(hipGetLastError());
+}
+
+static int32_t sample_morton(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
+                             float* rays, float* target, void* workspace, size_t ws_bytes, const UniK& u,
+                             hipStream_t stream);
+
 extern "C" int32_t hn_sample_rays_morton(const hn_ray_sampler* s, const float* image, const float* c2w,
                                          int64_t n_rays, float* rays, float* target, void* workspace,
                                          size_t ws_bytes, void* stream) {
+  UniK u;
+  make_uni(0, nullptr, 0, u);
+  return sample_morton(s, image, c2w, n_rays, rays, target, workspace, ws_bytes, u, (hipStream_t)stream);
+}
+
+extern "C" int32_t hn_sample_batch_morton(const hn_ray_sampler* s, const float* image, const float* c2w,
+                                          int64_t n_rays, float* rays, float* target, void* workspace,
+                                          size_t ws_bytes, uint64_t seed, const hn_uniform_draw* draws,
+                                          int32_t n_draws, void* stream) {
+  UniK u;
+  const int32_t st = make_uni(seed, draws, n_draws, u);
+  if (st) return st;
+  return sample_morton(s, image, c2w, n_rays, rays, target, workspace, ws_bytes, u, (hipStream_t)stream);
+}
+
+static int32_t sample_morton(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
+                             float* rays, float* target, void* workspace, size_t ws_bytes, const UniK& u,
+                             hipStream_t stream) {
   if (!s) return HN_E_NULL;
   if (n_rays < 0) return HN_E_SHAPE;
   if (n_rays == 0) return HN_OK;
@@ -360,8 +457,9 @@ extern "C" int32_t hn_sample_rays_morton(const hn_ray_sampler* s, const float* i
   int bits = 2;
   while ((1ull << bits) < M) bits += 2;
   int* counts = static_cast<int*>(workspace);
-  hipLaunchKernelGGL(morton_count_kernel, dim3(blocks), dim3(kMortonThreads), 0, (hipStream_t)stream, *s, bits / 2,
-                     n_rays, n_idx, counts);
+  const unsigned ublocks = (unsigned)((u.start[u.n] + kMortonThreads - 1) / kMortonThreads);
+  hipLaunchKernelGGL(morton_count_kernel, dim3(blocks + ublocks), dim3(kMortonThreads), 0, (hipStream_t)stream, *s,
+                     bits / 2, n_rays, n_idx, counts, u, blocks);
   hipLaunchKernelGGL(morton_emit_kernel, dim3(blocks), dim3(kMortonThreads), 0, (hipStream_t)stream, *s, image, c2w,
                      bits / 2, n_rays, n_idx, counts, rays, target);
   return hip_status(hipGetLastError());

@@ -438,7 +438,53 @@ class RenderRaysFn(torch.autograd.Function):
 # --------------------------------------------------------------------------
 # training-step driver (run_nerf.py:576-636)
 # --------------------------------------------------------------------------
-def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1):
+def _uniform_draws(shapes, dev):
+    """torch.rand(shape, device=dev) for each shape, as hn_uniform_draw
+    records: the default generator's seed, each draw's philox offset and
+    torch's thread count for its size (ATen calc_execution_policy: 256-thread
+    blocks, at most CUs x 2048 / 256 of them, 4 values per thread and call);
+    the generator is advanced as the torch.rand calls would advance it.
+    Returns (seed, ctypes array, output tensors)."""
+    if len(shapes) > L.UNIFORM_MAX_DRAWS:
+        raise ValueError(f"hashnerf_amd: at most {L.UNIFORM_MAX_DRAWS} uniform draws per launch")
+    dev = torch.device(dev)
+    torch.cuda.init()                          # default_generators is filled lazily
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    gen = torch.cuda.default_generators[idx]
+    props = _DEV_PROPS.get(idx)
+    if props is None:
+        p = torch.cuda.get_device_properties(idx)
+        props = _DEV_PROPS[idx] = (p.multi_processor_count,
+                                   getattr(p, "max_threads_per_multi_processor", 2048))
+    max_blocks = props[0] * (props[1] // 256)
+    seed, off = gen.initial_seed(), gen.get_offset()
+    arr = (L.HnUniformDraw * len(shapes))()
+    outs = []
+    for d, shape in zip(arr, shapes):
+        t = torch.empty(shape, dtype=torch.float32, device=dev)
+        n = t.numel()
+        threads = 256 * min((n + 255) // 256, max_blocks)
+        d.out, d.numel, d.threads, d.offset = t.data_ptr(), n, max(threads, 1), off
+        if n:
+            off += ((n - 1) // (threads * 4) + 1) * 4
+        outs.append(t)
+    gen.set_offset(off)
+    return seed & ((1 << 64) - 1), arr, outs
+
+
+_DEV_PROPS = {}
+
+
+def torch_uniform(shapes, dev):
+    """torch.rand(shape, device=dev) for every shape, bitwise, in one HIP
+    launch (hn_uniform_philox); the default generator ends where the torch.rand
+    calls would leave it."""
+    seed, arr, outs = _uniform_draws(shapes, dev)
+    L.check(L.lib().hn_uniform_philox(seed, arr, len(shapes), L.stream(torch.device(dev))), "uniform_philox")
+    return outs
+
+
+def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1, uniforms=None):
     """N_rand distinct pixels of one image (device, no replacement) -> the
     [n, 11] ray batch render() builds and the [n, 3] target colours.
     image [H, W, 3], c2w [3, 4] (or [4, 4]) fp32 on the device; crop =
@@ -447,7 +493,9 @@ def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1):
     of its pixels -- the batch order changes the loss and its gradient only
     by float summation order -- so the fused forward's XCD-contiguous ray
     groups are spatially coherent; order=0 (hn_sample_rays) keeps the draw
-    order.  Both are deterministic for a given seed."""
+    order.  Both are deterministic for a given seed.  uniforms: shapes of
+    torch.rand draws to make as well (torch_uniform; with order=1 in the
+    sampler's first launch), returned after rays and target."""
     L.require_device(image, c2w)
     image, c2w = image.contiguous(), c2w[:3, :4].contiguous()
     H, W = image.shape[0], image.shape[1]
@@ -465,6 +513,12 @@ def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1):
         if nb == 0:
             raise ValueError(f"sample_rays(order=1): window {s.crop_h}x{s.crop_w} too large")
         ws = _sampler_ws(dev, nb)
+        if uniforms:
+            useed, arr, outs = _uniform_draws(uniforms, dev)
+            L.check(L.lib().hn_sample_batch_morton(s, L.ptr(image), L.ptr(c2w), n_rays, L.ptr(rays),
+                                                   L.ptr(target), L.ptr(ws), nb, useed, arr, len(uniforms),
+                                                   L.stream(dev)), "sample_batch_morton")
+            return (rays, target, *outs)
         L.check(L.lib().hn_sample_rays_morton(s, L.ptr(image), L.ptr(c2w), n_rays, L.ptr(rays), L.ptr(target),
                                               L.ptr(ws), nb, L.stream(dev)), "sample_rays_morton")
     elif order == 0:
@@ -472,6 +526,8 @@ def sample_rays(image, c2w, n_rays, K, near, far, crop, seed, order=1):
                                        L.stream(dev)), "sample_rays")
     else:
         raise ValueError(f"sample_rays: order {order!r}")
+    if uniforms:
+        return (rays, target, *torch_uniform(uniforms, dev))
     return rays, target
 
 

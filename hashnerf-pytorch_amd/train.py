@@ -608,17 +608,25 @@ class Trainer:
             self.i_batch = 0
         return rays, target
 
-    def _draw_rays(self, i: int):
+    def _draw_rays(self, i: int, uniforms=None):
         """The step's rays and targets: the shuffled pool (use_batching) or
         N_rand pixels of one training image (device sampler, centre crop
-        before precrop_iters)."""
+        before precrop_iters).  uniforms = per-ray counts of torch.rand draws
+        on the default generator to make as well ([B, n] each, bitwise
+        torch's: functional.torch_uniform, inside the sampler's launch),
+        returned after rays and target."""
         if self.use_batching:
-            return self._pool_draw()
+            rays, target = self._pool_draw()
+            if uniforms:
+                B = rays.shape[0]
+                return (rays, target, *HF.torch_uniform([(B, n) for n in uniforms], self.device))
+            return rays, target
         a, d = self.args, self.data
         img_i = self._train_image()
         crop = self.crop if i < a.precrop_iters else (0, 0, d.H, d.W)
         return HF.sample_rays(d.images[img_i], d.poses[img_i], a.N_rand, d.K, 2., 6., crop,
-                              _step_seed(self.seed, self.rank, i), order=self.ray_order)
+                              _step_seed(self.seed, self.rank, i), order=self.ray_order,
+                              uniforms=[(a.N_rand, n) for n in uniforms] if uniforms else None)
 
     def sample_rays(self, i: int):
         """run_nerf.py:576-605 on the device: one image, N_rand pixels."""
@@ -734,15 +742,20 @@ class Trainer:
         Returns a dict rays [B, 11], target [B, 3], t_rand, u, tv (or None)."""
         a, d, kw = self.args, self.data, self.kw_train
         i = self.global_step + 1 if i is None else i
-        rays, target = self._draw_rays(i)
-        B = rays.shape[0]
         perturb = kw.get("perturb", 0.) > 0.
         # two draws in render_rays' order (run_nerf_helpers.py:528, then :276 via :548): the
         # autograd and reference-path modes draw them the same way, so all
-        # modes see the same numbers for the same device RNG state
-        t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
-        u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
-             torch.linspace(0., 1., kw["N_importance"], device=self.device).expand(B, kw["N_importance"]))
+        # modes see the same numbers for the same device RNG state.  On the
+        # device they are torch.rand restated bit for bit and made in the
+        # sampler's first launch (one launch instead of three)
+        if perturb and self.device.type == "cuda":
+            rays, target, t_rand, u = self._draw_rays(i, uniforms=(kw["N_samples"], kw["N_importance"]))
+        else:
+            rays, target = self._draw_rays(i)
+            B = rays.shape[0]
+            t_rand = torch.rand((B, kw["N_samples"]), device=self.device) if perturb else None
+            u = (torch.rand((B, kw["N_importance"]), device=self.device) if perturb else
+                 torch.linspace(0., 1., kw["N_importance"], device=self.device).expand(B, kw["N_importance"]))
         tv = None
         if a.tv_loss_weight > 0 and self.rank == 0 and i <= a.tv_until:
             tv = draw_tv_cubes(self.embed_fn.n_levels, self.embed_fn.base_resolution,

@@ -332,6 +332,28 @@ size_t hn_sample_rays_morton_workspace_bytes(const hn_ray_sampler* s);
 int32_t hn_sample_rays_morton(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
                               float* rays, float* target, void* workspace, size_t ws_bytes, void* stream);
 
+/* ABI 13: torch.rand on the device's default generator, restated bit for bit
+ * (render_rays' draws, run_nerf_helpers.py:528 t_rand and :276 via :548 u):
+ * ATen's uniform_ kernel runs `threads` = blockDim x gridDim threads of
+ * hiprand Philox4x32-10 (key = seed, subsequence = thread, counter = offset / 4
+ * + call), four values per call, element li from thread li % threads, call
+ * li / (4 threads), component (li / threads) % 4; value 2^-32 + v 2^-32, with
+ * 1 mapped to 0.  The caller supplies the generator's seed and each draw's
+ * offset and threads as torch would use them (and advances the generator). */
+typedef struct hn_uniform_draw {
+  float* out;               /* [numel] */
+  int64_t numel;
+  int64_t threads;          /* torch's launch for this numel: 256 x min(ceil(numel / 256), CUs x 2048 / 256) */
+  uint64_t offset;          /* the generator's philox offset at this draw (a multiple of 4) */
+} hn_uniform_draw;
+#define HN_UNIFORM_MAX_DRAWS 4
+int32_t hn_uniform_philox(uint64_t seed, const hn_uniform_draw* draws, int32_t n_draws, void* stream);
+/* hn_sample_rays_morton with the step's uniform draws made in its first
+ * launch (one launch less than the sampler + torch.rand's own launches). */
+int32_t hn_sample_batch_morton(const hn_ray_sampler* s, const float* image, const float* c2w, int64_t n_rays,
+                               float* rays, float* target, void* workspace, size_t ws_bytes, uint64_t seed,
+                               const hn_uniform_draw* draws, int32_t n_draws, void* stream);
+
 /* use_batching ray pool (run_nerf.py:505-521 builds rays_rgb from every training
  * pixel and shuffles it; :544-555 takes consecutive N_rand slices and reshuffles
  * after each epoch).  The pool is never materialised: position q of an epoch

@@ -336,3 +336,45 @@ def test_trainer_fused_loss_same_trajectory(hn):
         assert torch.equal(a[k], b[k]), k
     for x, y in zip(a[4], b[4]):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("shapes", [[(4096, 64), (4096, 128)], [(1000, 7)], [(3, 2_500_001), (17,)],
+                                    [(8192, 64), (0, 5), (8192, 128)]])
+def test_uniform_philox_matches_torch_rand(hn, shapes):
+    """functional.torch_uniform (hn_uniform_philox, ABI 13) = torch.rand on
+    the default generator, bit for bit, and leaves the generator's offset
+    where the torch.rand calls leave it: the trainer's two draws, a ragged
+    size, one big enough that torch's threads loop (components 1-3 and later
+    Philox calls used), an empty draw between two."""
+    from hashnerf_pytorch_amd import functional as HF
+    torch.cuda.init()
+    gen = torch.cuda.default_generators[torch.cuda.current_device()]
+    torch.cuda.manual_seed(1234)
+    torch.rand(5, device=DEV)                  # a nonzero starting offset
+    off0 = gen.get_offset()
+    ref = [torch.rand(s, device=DEV) for s in shapes]
+    off_ref = gen.get_offset()
+    gen.set_offset(off0)
+    got = HF.torch_uniform(shapes, DEV)
+    assert gen.get_offset() == off_ref
+    for r, g in zip(ref, got):
+        assert r.shape == g.shape and torch.equal(r, g)
+    assert torch.equal(torch.rand(9, device=DEV), (gen.set_offset(off_ref), torch.rand(9, device=DEV))[1])
+
+
+def test_sample_batch_morton_draws(hn):
+    """sample_rays(uniforms=...) (hn_sample_batch_morton): the same rays and
+    targets as hn_sample_rays_morton and the same numbers as two torch.rand
+    calls after it, from one launch pair."""
+    from hashnerf_pytorch_amd import functional as HF
+    from hashnerf_pytorch_amd.train import SyntheticBlender
+    d = SyntheticBlender(200, 200, 2, DEV, seed=0)
+    args = (d.images[0], d.poses[0], 4096, d.K, 2., 6., (0, 0, 200, 200), 77)
+    torch.cuda.manual_seed(9)
+    r0, t0 = HF.sample_rays(*args)
+    a = torch.rand((4096, 64), device=DEV)
+    b = torch.rand((4096, 128), device=DEV)
+    torch.cuda.manual_seed(9)
+    r1, t1, a1, b1 = HF.sample_rays(*args, uniforms=[(4096, 64), (4096, 128)])
+    for x, y in ((r0, r1), (t0, t1), (a, a1), (b, b1)):
+        assert torch.equal(x, y)
