@@ -306,6 +306,8 @@ def main():
                     help="A/B: draw the next step's batch on a side stream beside the backward")
     ap.add_argument("--separate-loss", action="store_true",
                     help="A/B: the loss in its own hn_loss_fwd_bwd launch instead of the backward's pre-pass")
+    ap.add_argument("--separate-mlp-step", action="store_true",
+                    help="A/B: the MLP RAdam step in its own hn_radam_step launch")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -370,6 +372,7 @@ def main():
     # waits cost more than the ~20 us of sampler and RNG launches they move
     tr.prefetch = args.prefetch
     tr.fuse_loss = not args.separate_loss
+    tr.fuse_mlp_step = not args.separate_mlp_step
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1

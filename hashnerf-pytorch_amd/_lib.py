@@ -80,7 +80,7 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
                 ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
                 ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32),
-                ("loss", C.POINTER(HnRenderLoss))]
+                ("loss", C.POINTER(HnRenderLoss)), ("mlp_step", C.POINTER(HnRadamTensor))]
 
 
 class HnTvArgs(C.Structure):

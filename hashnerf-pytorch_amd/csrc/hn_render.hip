@@ -1489,8 +1489,12 @@ constexpr int kSlabIlp = 8;   // slab loads in flight per thread (a power of 2)
 // element is fixed (the group partials, then the pairwise combines), so the
 // sums are the same whichever kernel runs it (slab_reduce_kernel, or the
 // binned scatter's tail).  1024 threads; part[16][64] in LDS.
+// ms (binned scatter, optional): the ten NeRFSmall tensors' RAdam steps
+// ([network_fn's 5 | network_fine's 5], hn_mlp order), applied to each element
+// with its final gradient (radam_kernel's update) where that is formed.
 HN_DEV void slab_reduce_block(const float* __restrict__ slab, int n_blocks, const hn_mlp_grad& dc,
-                              const hn_mlp_grad& df, int overwrite, int vblock, float (*part)[64]) {
+                              const hn_mlp_grad& df, int overwrite, int vblock, float (*part)[64],
+                              const hn_radam_tensor* ms = nullptr) {
   const int lane = threadIdx.x & 63;
   const int e = vblock * 64 + lane;
   const int grp = threadIdx.x >> 6;
@@ -1531,13 +1535,19 @@ HN_DEV void slab_reduce_block(const float* __restrict__ slab, int n_blocks, cons
       for (int g = 0; g < w; ++g) t[g] = t[g] + t[g + w];
     s = t[0];
     const hn_mlp_grad& d = fine ? df : dc;
-    float* dst;
-    if (i < W_S1) dst = d.sigma0 + i;
-    else if (i < W_C0) dst = d.sigma1 + (i - W_S1);
-    else if (i < W_C1) dst = d.color0 + (i - W_C0);
-    else if (i < W_C2) dst = d.color1 + (i - W_C1);
-    else dst = d.color2 + (i - W_C2);
-    *dst = overwrite ? s : *dst + s;
+    const int ly = i < W_S1 ? 0 : i < W_C0 ? 1 : i < W_C1 ? 2 : i < W_C2 ? 3 : 4;   // the torch tensor
+    const int j = i - (ly == 0 ? 0 : ly == 1 ? W_S1 : ly == 2 ? W_C0 : ly == 3 ? W_C1 : W_C2);
+    float* dst = (ly == 0 ? d.sigma0 : ly == 1 ? d.sigma1 : ly == 2 ? d.color0 : ly == 3 ? d.color1 : d.color2) + j;
+    const float gv = overwrite ? s : *dst + s;
+    *dst = gv;
+    if (ms) {
+      const hn_radam_tensor& r = ms[(fine ? 5 : 0) + ly];
+      float p = r.p[j], m = r.m[j], v = r.v[j];
+      radam_elem(r, p, gv, m, v);
+      r.m[j] = m;
+      r.v[j] = v;
+      if (r.mode != 0) r.p[j] = p;
+    }
   }
 }
 constexpr int kSlabVBlocks = (2 * W_END + 63) / 64;
@@ -1564,6 +1574,8 @@ struct ScK {
   int32_t overwrite_mlp;
   int32_t merge_levels;    // levels 0 .. merge_levels-1: records merged per block (merge table)
   int32_t mh_log2;         // log2 merge-table slots (sc_lds_bytes)
+  int32_t has_mstep;       // the NeRFSmall tensors' RAdam steps run in the slab reduction (mstep)
+  hn_radam_tensor mstep[10];
 };
 constexpr int kScWaves = 16;
 constexpr int kScMaxBinsLog2 = 13;
@@ -2065,7 +2077,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       __syncthreads();
       const int vb = vb_sh;
       if (vb >= kSlabVBlocks) break;
-      slab_reduce_block(k.slab, kBwdBlocks, k.dc, k.df, k.overwrite_mlp, vb, part);
+      slab_reduce_block(k.slab, kBwdBlocks, k.dc, k.df, k.overwrite_mlp, vb, part, k.has_mstep ? k.mstep : nullptr);
     }
   }
 }
@@ -3248,6 +3260,15 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     }
   }
   if (a->owner_defer && mode != kModeSplit) return HN_E_SHAPE;
+  if (a->mlp_step) {   // the MLP steps live in the binned scatter's slab reduction
+    if (mode != kModeSplit) return HN_E_SHAPE;
+    static constexpr int64_t numel[5] = {W_S1, W_C0 - W_S1, W_C1 - W_C0, W_C2 - W_C1, W_END - W_C2};
+    for (int t = 0; t < 10; ++t) {
+      const hn_radam_tensor& r = a->mlp_step[t];
+      if (!r.p || !r.m || !r.v) return HN_E_NULL;
+      if (r.n != numel[t % 5]) return HN_E_SHAPE;
+    }
+  }
   const WsLayout wl = ws_layout(cfg, a->n_rays, mode);
   BinGeom bg{};
   k.bins = nullptr;
@@ -3309,6 +3330,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
     sk.merge_levels = merge_levels(cfg);
     sk.mh_log2 = sc_mh_log2(sk.nbins, sk.merge_levels);
+    sk.has_mstep = a->mlp_step != nullptr;
+    for (int t = 0; t < 10; ++t) sk.mstep[t] = sk.has_mstep ? a->mlp_step[t] : hn_radam_tensor{};
     const size_t sc_lds = sc_lds_bytes(sk.nbins, sk.mh_log2);
     if (sc_lds + sc_static_lds() > kLdsMax) return HN_E_SHAPE;   // bins beyond the LDS counters' room
     hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), sc_lds, s, sk);

@@ -274,7 +274,8 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
 
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
-               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False, loss=None):
+               overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False, loss=None,
+               mlp_step=None):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -298,7 +299,10 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     None, world, sparse_w, tv_w) forms the training loss's upstream
     gradients in the backward itself (run_nerf.py:612-636 under
     train.dp_loss's rule; grads is not read) and writes out = loss, mse,
-    mse0, entropy sum (loss_fwd's)."""
+    mse0, entropy sum (loss_fwd's).
+    mlp_step (binned scatter): the ten (p, exp_avg, exp_avg_sq, coeffs) of
+    RAdam.take_step for st.ws's tensors, applied where each weight's final
+    gradient is formed (the slab reduction; dws is still written)."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -352,6 +356,20 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
         keep.append(g_tv)
         a.g_tv = g_tv.data_ptr()
     a.owner_defer = 1 if owner_defer else 0
+    if mlp_step is not None:
+        if len(mlp_step) != 10:
+            raise ValueError("hashnerf_amd.render_bwd: mlp_step needs the ten NeRFSmall tensors' steps")
+        ms = (L.HnRadamTensor * 10)()
+        for d, (p, m, v, c), w in zip(ms, mlp_step, st.ws):
+            if p.data_ptr() != w.data_ptr():
+                raise ValueError("hashnerf_amd.render_bwd: mlp_step must follow the render's weights in order")
+            L.require_device(p, m, v)
+            d.p, d.g, d.m, d.v, d.n = p.data_ptr(), None, m.data_ptr(), v.data_ptr(), p.numel()
+            for k in ("beta1", "beta2", "one_minus_beta1", "one_minus_beta2", "eps", "neg_wd_lr", "neg_step_lr",
+                      "mode", "has_wd"):
+                setattr(d, k, c[k])
+        a.mlp_step = ms
+        keep.append(ms)
     if loss is not None:
         la = L.HnRenderLoss()
         ts = [L.contig(loss[k]) for k in ("target", "rgb", "rgb0", "sparsity", "sparsity0")]

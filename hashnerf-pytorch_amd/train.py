@@ -576,6 +576,9 @@ class Trainer:
         # cross-stream waits cost more than the launches they move), so off
         # unless asked for (bench.py --prefetch).
         self.prefetch = False
+        # one GPU, fused table step: the MLP tensors' RAdam steps run in the
+        # backward's slab reduction too (no hn_radam_step launch)
+        self.fuse_mlp_step = True
         self._pf = None          # (step, batch, ready event) drawn ahead
         # explicit mode: the loss value and its gradients formed by the render
         # backward's composite pre-pass (ABI 13) instead of an hn_loss_fwd_bwd
@@ -843,8 +846,11 @@ class Trainer:
             # binned owner pass forms it, so the table's RAdam step runs there
             # (run_nerf.py:642 for the embedding group) and the gradient is
             # never stored; optimizer.step() then updates the MLP groups only
+            # the MLP groups' steps likewise, where the slab reduction forms
+            # their gradients (optimizer.step() then has nothing left)
+            mstep = [self.optimizer.take_step(p) for p in self._ws] if self.fuse_mlp_step else None
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), loss=loss)
+                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), loss=loss, mlp_step=mstep)
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:

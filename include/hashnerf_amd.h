@@ -258,6 +258,11 @@ typedef struct hn_render_bwd_args {
    * The workspace must not be touched in between. */
   int32_t owner_defer;
   const hn_render_loss* loss;   /* ABI 13: NULL, or the training loss formed here (above) */
+  const struct hn_radam_tensor* mlp_step;   /* ABI 13 (binned scatter only, else HN_E_SHAPE): NULL, or [10] the
+                               NeRFSmall tensors' RAdam steps (network_fn's sigma_net.0, sigma_net.1,
+                               color_net.0, color_net.1, color_net.2, then network_fine's; g unused),
+                               applied where each weight's final gradient is formed (hn_radam_step's
+                               per-element update; the gradient is still written to d_coarse / d_fine) */
 } hn_render_bwd_args;
 
 /* The binned scatter's bins for this cfg and batch: returns their number (0:

@@ -378,3 +378,32 @@ def test_sample_batch_morton_draws(hn):
     r1, t1, a1, b1 = HF.sample_rays(*args, uniforms=[(4096, 64), (4096, 128)])
     for x, y in ((r0, r1), (t0, t1), (a, a1), (b, b1)):
         assert torch.equal(x, y)
+
+
+def test_trainer_fused_mlp_step_same_trajectory(hn):
+    """Trainer.fuse_mlp_step (ABI 13: the ten NeRFSmall RAdam steps applied in
+    the backward's slab reduction, hn_render_bwd_args.mlp_step) against
+    optimizer.step()'s hn_radam_step launch: 8 steps (the first five in
+    RAdam's no-update mode, TV through step 5) leave the table, every weight
+    and every moment bitwise equal."""
+    from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
+    data = SyntheticBlender(64, 64, 4, DEV, seed=0)
+    res = {}
+    for fm in (False, True):
+        args = default_args(N_rand=512, log2_hashmap_size=14, tv_loss_weight=1e-4, tv_until=5,
+                            sparse_loss_weight=1e-3)
+        tr = Trainer(args, data, DEV, seed=3)
+        tr.fuse_mlp_step = fm
+        torch.manual_seed(11)
+        losses = [float(tr.step()[0]) for _ in range(8)]
+        ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
+        st = [tr.optimizer.state[p] for p in ws]
+        res[fm] = (losses, tr.embed_fn.table.detach().clone(), [p.detach().clone() for p in ws],
+                   [s["exp_avg"].clone() for s in st], [s["exp_avg_sq"].clone() for s in st],
+                   [int(s["step"]) for s in st])
+    a, b = res[False], res[True]
+    assert a[0] == b[0] and a[5] == b[5]
+    assert torch.equal(a[1], b[1])
+    for k in (2, 3, 4):
+        for x, y in zip(a[k], b[k]):
+            assert torch.equal(x, y), k
