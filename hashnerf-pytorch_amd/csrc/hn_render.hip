@@ -930,9 +930,6 @@ HN_DEV void c0sh_seed(const C0Sh& c, f32x16 (&c0)[2], int h) {
     }
 }
 
-#ifndef HN_B1_WGX   // 1: weight-gradient products inside the next data-path GEMM (WgX)
-#define HN_B1_WGX 1
-#endif
 // One 32-point tile: recompute the forward (features from the cache), then
 // the MLP backward; dW into the wave's accumulators, d feature to dst.
 HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f32x16& feat,
@@ -972,11 +969,11 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
     }
   }
   tile_lds_order();
-#if HN_B1_WGX
   // Each layer's weight-gradient products run inside the NEXT data-path GEMM
   // (WgX): its operands are read here, before that GEMM's image writes, and
   // its MFMAs fill the chain's gaps -- per accumulator the same products in
-  // the same order as the wgrad_n form below (bitwise-equal dW).
+  // the same order as the separate wgrad_n form of round 4 (bitwise-equal dW;
+  // step 0.988 -> 0.980 ms, r05i).
   // ---- color_net.2 (dW rows >= 3 are discarded) inside color_net.2^T ----
   WgOps<1, 2> w_c2;
   {
@@ -1023,49 +1020,6 @@ HN_DEV f32x16 b1_tile(const float* __restrict__ P, WRing& wr, float* X, const f3
   }
   const f32x16 dfeat = gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; },
                                                   Xb, WgX<1, 2, 4>{w_s1, dw.s1});
-#else
-  // ---- color_net.2 (dW rows >= 3 are discarded) ----
-  {
-    const int ab[1] = {kBDR}, bb[2] = {kBC1, kBC1 + 1};
-    wgrad_n<1, 2>(Xb, ab, bb, dw.c2, lane);
-  }
-  const float dy2[2] = {h ? dr.y : dr.x, h ? 0.f : dr.z};
-  f32x16 dc1[2] = {zero16(), zero16()};
-  gemm2<R_B4>(wr, P, dc1, lane, [&](int s) { return s < 2 ? dy2[s] : 0.f; });
-  mask_bits(dc1[0], mc1, 0);
-  mask_bits(dc1[1], mc1, 1);
-  // ---- color_net.1 (dc1 image over c1) ----
-  f32x16 dc0[2] = {zero16(), zero16()};
-  gemm2<R_B3, kBC1>(wr, P, dc0, lane, [&](int s) { return dc1[s >> 4][s & 15]; }, Xb);
-  mask_bits(dc0[0], mc0, 0);
-  mask_bits(dc0[1], mc0, 1);
-  tile_lds_order();
-  {
-    const int ab[2] = {kBC1, kBC1 + 1}, bb[2] = {kBC0, kBC0 + 1};
-    wgrad_n<2, 2>(Xb, ab, bb, dw.c1, lane);     // dw.c1[2 * nb + kb]
-  }
-  // ---- color_net.0 (dc0 image over c0; B = [sh16 | sigma | geo15]) ----
-  f32x16 ds1 = gemm_w<seg_of(R_B2G), kBC0>(wr, P, zero16(), lane, [&](int s) { return dc0[s >> 4][s & 15]; }, Xb);
-  if (h == 0) ds1[0] = dr.w;                    // row 0 = sigma (A row 0 is zero)
-  tile_lds_order();
-  {
-    const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBC0in};
-    wgrad_n<2, 1>(Xb, ab, bb, dw.c0, lane);
-  }
-  // ---- sigma_net.1 (ds1 image over dc1's first tile; rows 16..31 discarded) ----
-  f32x16 dh0[2] = {zero16(), zero16()};
-  gemm2<R_B1, kBC1>(wr, P, dh0, lane, [&](int s) { return ds1[s]; }, Xb);
-  mask_bits(dh0[0], mh0, 0);
-  mask_bits(dh0[1], mh0, 1);
-  tile_lds_order();
-  {
-    const int ab[1] = {kBC1}, bb[2] = {kBH0, kBH0 + 1};
-    wgrad_n<1, 2>(Xb, ab, bb, dw.s1, lane);
-  }
-  // ---- sigma_net.0 (dh0 image over dc0) ----
-  const f32x16 dfeat =
-      gemm_w<seg_of(R_B0), kBC0>(wr, P, zero16(), lane, [&](int s) { return dh0[s >> 4][s & 15]; }, Xb);
-#endif
   tile_lds_order();
   {
     const int ab[2] = {kBC0, kBC0 + 1}, bb[1] = {kBF};
@@ -1645,12 +1599,10 @@ HN_DEV StPhase st_phase(int l, int log2T, int shift, int lg2n = 0) {
   ph.log2c = kStLog2 - lg - lg2n;
   return ph;
 }
-#ifndef HN_SC_PF   // the next level's grads loaded while a level runs
-#define HN_SC_PF 0
-#endif
-#ifndef HN_SC_LPP   // log2 levels per staging phase (one block barrier pair per phase)
-#define HN_SC_LPP 1
-#endif
+// log2 levels per staging phase where the pool still holds 8 records per bin
+// (one block barrier pair per phase; r05h: 1 level 0.984-0.987 ms per step,
+// 2: 0.988-1.005, 4: 1.012-1.014, 8: 1.037-1.039)
+constexpr int kScLpp = 1;
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // dynamic LDS: the bins' record counters, then the staging pool / merge
@@ -1764,28 +1716,20 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   };
   // level l's grads = elements 2 (l & 1) .. of level pair l / 2 (tile_level:
   // chunk lp / 2 of lane half lp % 2); a coarse twin adds its coarse grads
-  // a level's grads as two loads (fine, coarse twin) issued ahead of their
-  // use (grads_take): the staged loop loads level l + 1's while level l runs
-  struct GradLd {
-    float2 f, t;
-  };
-  auto grads_issue = [&](const Unit& q, int l) {
-    GradLd gl{make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-    if (!q.act) return gl;
-    const int lp = l >> 1, o = 4 * (64 * (lp >> 1) + 32 * (lp & 1)) + 2 * (l & 1);
-    gl.f = *reinterpret_cast<const float2*>(q.tb + o);
-    if (q.tw) gl.t = *reinterpret_cast<const float2*>(q.tw + o);
-    return gl;
-  };
-  auto grads_take = [&](Unit& q, const GradLd& gl) {
+  // (the fused ring's order); no twin: the fine grads as they are.  (Loading
+  // level l + 1's while level l runs measured no faster, r05g.)
+  auto unit_grads = [&](Unit& q, int l) {
     if (!q.act) return;
-    // fine + coarse twin (the fused ring's order); no twin: the fine grads as they are
-    const float2 gq = q.tw ? make_float2(gl.f.x + gl.t.x, gl.f.y + gl.t.y) : gl.f;
+    const int lp = l >> 1, o = 4 * (64 * (lp >> 1) + 32 * (lp & 1)) + 2 * (l & 1);
+    float2 gq = *reinterpret_cast<const float2*>(q.tb + o);
+    if (q.tw) {
+      const float2 t = *reinterpret_cast<const float2*>(q.tw + o);
+      gq = make_float2(gq.x + t.x, gq.y + t.y);
+    }
     q.g0 = gq.x;
     q.g1 = gq.y;
     bad |= !(fabsf(gq.x + gq.y) <= 3.402823466e38f);
   };
-  auto unit_grads = [&](Unit& q, int l) { grads_take(q, grads_issue(q, l)); };
   auto unit_at = [&](int64_t it, int l) {
     Unit q = unit_base(it);
     unit_grads(q, l);
@@ -1929,7 +1873,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // pool still holds >= 2^kStMinLog2C records per bin (T=19: 2 levels per
   // phase, 32 records per bin; T=22: 1 level, 8 per bin)
   const int lg_bins = log2T - sh;   // log2 bins per level
-  const int lpp = lg_bins < 0 ? 0 : max(0, min(HN_SC_LPP, kStLog2 - kStMinLog2C - lg_bins));
+  const int lpp = lg_bins < 0 ? 0 : max(0, min(kScLpp, kStLog2 - kStMinLog2C - lg_bins));
   auto phase_of = [&](int l) { return st_phase(l, log2T, sh, l + (1 << lpp) <= 16 ? lpp : 0); };
   if (n_merge < 16) st_init(phase_of(n_merge), par);
   __syncthreads();
@@ -1982,19 +1926,11 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // their records through the staging pool, one phase per (unit round, level)
   for (int64_t it = 0; it < n_it && n_merge < 16; ++it) {
     Unit q = unit_base(it);
-#if HN_SC_PF
-    GradLd gl = grads_issue(q, n_merge);
-#endif
     for (int l = n_merge; l < 16;) {
       const StPhase ph = phase_of(l);
       const int np = l + (1 << lpp) <= 16 ? 1 << lpp : 1;
       for (int j = 0; j < np; ++j, ++l) {
-#if HN_SC_PF
-        grads_take(q, gl);
-        if (l + 1 < 16) gl = grads_issue(q, l + 1);   // in flight across this level's work
-#else
         unit_grads(q, l);
-#endif
         level(q, l, kStaged, 1.f, ph);
       }
       __syncthreads();   // the phase's records are in the pool, its counts final
@@ -2683,10 +2619,7 @@ HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_
 // ids through LDS cursors (spilled records clump into few bins: per-record
 // global cursors serialise on them).  Returns at once when nothing spilled
 // (the usual case).
-#ifndef HN_PLACE_THREADS
-#define HN_PLACE_THREADS 1024
-#endif
-constexpr int kPlaceThreads = HN_PLACE_THREADS;
+constexpr int kPlaceThreads = 1024;   // 256 measured the same (r05: the launch, not its work)
 __global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
   __shared__ uint32_t cur[kScMaxBins], lc[kScMaxBins];
   __shared__ uint32_t part[kPlaceThreads];
