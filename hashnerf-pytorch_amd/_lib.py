@@ -60,7 +60,7 @@ class HnRenderFwdArgs(C.Structure):
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
                 ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
-                ("fine_src", _P), ("feat", _P)]
+                ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32)]
 
 
 class HnRadamTensor(C.Structure):
@@ -80,7 +80,8 @@ class HnRenderBwdArgs(C.Structure):
                 ("g_raw_f", _P), ("d_table", _P), ("d_coarse", HnMlpGrad), ("d_fine", HnMlpGrad),
                 ("table_step", C.POINTER(HnRadamTensor)), ("tv", C.c_void_p), ("g_tv", _P),
                 ("table_live", _P), ("table_live_levels", C.c_int32), ("owner_defer", C.c_int32),
-                ("loss", C.POINTER(HnRenderLoss)), ("mlp_step", C.POINTER(HnRadamTensor))]
+                ("loss", C.POINTER(HnRenderLoss)), ("mlp_step", C.POINTER(HnRadamTensor)),
+                ("repack", C.c_int32)]
 
 
 class HnTvArgs(C.Structure):

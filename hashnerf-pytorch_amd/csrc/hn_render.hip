@@ -2620,7 +2620,19 @@ HN_DEV void bin_add(unsigned long long* acc, uint32_t se, const f32x4 v, uint32_
 // global cursors serialise on them).  Returns at once when nothing spilled
 // (the usual case).
 constexpr int kPlaceThreads = 1024;   // 256 measured the same (r05: the launch, not its work)
-__global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k) {
+// The stepped NeRFSmall weights' MFMA copies (hn_render_bwd_args.repack):
+// extra workgroups of the placement launch, which runs after the scatter
+// kernel's slab reduction has stepped every weight (mlp_pack2_kernel's values)
+struct PackK {
+  hn_mlp c, f;
+  float* P;   // [2][G_END]: the workspace's packed copies (hn_render_fwd's Pc, Pf)
+};
+__global__ __launch_bounds__(kPlaceThreads) void ovf_place_kernel(BinR k, PackK pk) {
+  if (blockIdx.x >= kBwdBlocks) {
+    const int idx = (int)(blockIdx.x - kBwdBlocks) * kPlaceThreads + (int)threadIdx.x;
+    if (idx < 2 * G_END) pk.P[idx] = idx < G_END ? pack_value(pk.c, idx) : pack_value(pk.f, idx - G_END);
+    return;
+  }
   __shared__ uint32_t cur[kScMaxBins], lc[kScMaxBins];
   __shared__ uint32_t part[kPlaceThreads];
   const size_t nrec = bin_records(k.nbins, k.cap, k.n_rays);
@@ -3024,7 +3036,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   hipStream_t s = (hipStream_t)stream;
   float* Pc = (float*)workspace;
   float* Pf = Pc + G_END;
-  if ((st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
+  if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   RenderK k;
   k.g = make_grid_args(cfg->grid);
   k.white = cfg->white_bkgd;
@@ -3193,6 +3205,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     }
   }
   if (a->owner_defer && mode != kModeSplit) return HN_E_SHAPE;
+  if (a->repack && !a->mlp_step) return HN_E_SHAPE;
   if (a->mlp_step) {   // the MLP steps live in the binned scatter's slab reduction
     if (mode != kModeSplit) return HN_E_SHAPE;
     static constexpr int64_t numel[5] = {W_S1, W_C0 - W_S1, W_C1 - W_C0, W_C2 - W_C1, W_END - W_C2};
@@ -3272,7 +3285,15 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   }
   if (mode != kModeAtomic) {
     const BinR r = owner_args(cfg, a, k.bins, bg, 0);
-    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r);
+    PackK pk{};
+    unsigned pblocks = 0;
+    if (a->repack) {   // checked above: mlp_step given, binned scatter
+      pk.c = a->coarse;
+      pk.f = a->fine;
+      pk.P = (float*)workspace;
+      pblocks = (unsigned)((2 * G_END + kPlaceThreads - 1) / kPlaceThreads);
+    }
+    hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks + pblocks), dim3(kPlaceThreads), 0, s, r, pk);
     if ((st = hip_status(hipGetLastError()))) return st;
     if (!a->owner_defer) {
       hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),

@@ -221,10 +221,13 @@ class RenderState:
                  "fine_src", "feat", "wsb", "nbytes", "bwd_args")
 
 
-def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None):
+def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None,
+               weights_packed=False):
     """hn_render_fwd (run_nerf_helpers.py:464-574, forward).  Returns the
     output dict and a RenderState (None when keep_feat is False).  wsb: the
-    caller's workspace (uint8, >= workspace_bytes; default a fresh one)."""
+    caller's workspace (uint8, >= workspace_bytes; default a fresh one);
+    weights_packed: it already holds ws's packed copies (render_bwd with
+    repack=True since the last change of ws)."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -258,6 +261,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
         raise ValueError(f"hashnerf_amd.render_fwd: wsb must be a contiguous buffer of >= {nbytes} bytes on {dev}")
     else:
         nbytes = wsb.numel() * wsb.element_size()
+    a.weights_packed = 1 if weights_packed else 0
     t0 = TIMER.begin("render_fwd")
     L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
     TIMER.end("render_fwd", t0)
@@ -275,7 +279,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
 
 def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = False, table_step=None,
                overwrite_mlp: bool = False, tv=None, table_live=None, owner_defer: bool = False, loss=None,
-               mlp_step=None):
+               mlp_step=None, repack: bool = False):
     """hn_render_bwd: accumulates (+=) d loss / d table into d_table (or
     writes it, overwrite=True: d_table need not be zeroed) and the ten
     NeRFSmall weight gradients into dws (coarse 5, fine 5, +=; written with
@@ -302,7 +306,9 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     mse0, entropy sum (loss_fwd's).
     mlp_step (binned scatter): the ten (p, exp_avg, exp_avg_sq, coeffs) of
     RAdam.take_step for st.ws's tensors, applied where each weight's final
-    gradient is formed (the slab reduction; dws is still written)."""
+    gradient is formed (the slab reduction; dws is still written); with
+    repack=True the stepped weights' packed copies are then written into the
+    workspace, for a next render_fwd(wsb=st.wsb, weights_packed=True)."""
     B = st.rays.shape[0]
     dev = st.rays.device
     a = L.HnRenderBwdArgs()
@@ -369,6 +375,7 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
                       "mode", "has_wd"):
                 setattr(d, k, c[k])
         a.mlp_step = ms
+        a.repack = 1 if repack else 0
         keep.append(ms)
     if loss is not None:
         la = L.HnRenderLoss()

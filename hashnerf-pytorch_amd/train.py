@@ -579,6 +579,10 @@ class Trainer:
         # one GPU, fused table step: the MLP tensors' RAdam steps run in the
         # backward's slab reduction too (no hn_radam_step launch)
         self.fuse_mlp_step = True
+        # ... and then repacks them for the next forward, which reuses the
+        # render workspace (kept across steps) instead of packing again
+        self._rws = None         # the render workspace
+        self._pk = None          # (workspace, weight versions) its packed copies belong to
         self._pf = None          # (step, batch, ready event) drawn ahead
         # explicit mode: the loss value and its gradients formed by the render
         # backward's composite pre-pass (ABI 13) instead of an hn_loss_fwd_bwd
@@ -811,7 +815,12 @@ class Trainer:
             cubes, mv0 = batch["tv"]
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
         consts = (self.world, a.sparse_loss_weight, a.tv_loss_weight)
-        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True)
+        nb = HF.L.lib().hn_render_workspace_bytes(self._cfg, rays.shape[0])
+        if self._rws is None or self._rws.numel() < nb:
+            self._rws, self._pk = torch.empty(nb, dtype=torch.uint8, device=self.device), None
+        out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True,
+                                wsb=self._rws, weights_packed=self._pk is not None and self._pk == self._pack_key())
+        self._pk = None
         if pf:
             self._prefetch(i + 1)
         loss = None
@@ -850,7 +859,10 @@ class Trainer:
             # their gradients (optimizer.step() then has nothing left)
             mstep = [self.optimizer.take_step(p) for p in self._ws] if self.fuse_mlp_step else None
             HF.render_bwd(st, grads, None, self._gws, table_step=self.optimizer.take_step(table),
-                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), loss=loss, mlp_step=mstep)
+                          overwrite_mlp=True, tv=tvb, table_live=self._live_mask(), loss=loss, mlp_step=mstep,
+                          repack=mstep is not None)
+            if mstep is not None:
+                self._pk = self._pack_key()   # the workspace holds the stepped weights' copies
             table.grad = None
         else:
             # the render backward writes every table-gradient entry (overwrite:
@@ -864,6 +876,12 @@ class Trainer:
         for p, g in zip(self._ws, self._gws):
             p.grad = g
         return lo[0], lo[1]
+
+    def _pack_key(self):
+        """What the workspace's packed weights must match: the buffer and
+        every weight's version counter (an in-place change of a weight, e.g.
+        a checkpoint load, bumps it; the HIP optimizer's writes do not)."""
+        return (self._rws.data_ptr(), tuple(p._version for p in self._ws))
 
     def _empty_rank_grads(self, batch):
         """A rank that drew no rays this step (world > 1, use_batching: the

@@ -203,6 +203,9 @@ typedef struct hn_render_fwd_args {
   float* feat;              /* [B][HN_RENDER_FEAT_PER_RAY] hash features of the 64 + 192
                                evaluated points and their ReLU masks (MFMA-tile order,
                                opaque); NULL = not kept (inference); required by hn_render_bwd */
+  int32_t weights_packed;   /* ABI 13: nonzero = `workspace` already holds both nets' packed MFMA
+                               copies of these weights (an hn_render_bwd with repack wrote them and the
+                               weights are unchanged since): no packing launch */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
@@ -263,6 +266,9 @@ typedef struct hn_render_bwd_args {
                                color_net.0, color_net.1, color_net.2, then network_fine's; g unused),
                                applied where each weight's final gradient is formed (hn_radam_step's
                                per-element update; the gradient is still written to d_coarse / d_fine) */
+  int32_t repack;           /* ABI 13, with mlp_step: then write the stepped weights' packed MFMA copies
+                               into `workspace` (in the overflow-placement launch), so the next
+                               hn_render_fwd on this workspace may set weights_packed */
 } hn_render_bwd_args;
 
 /* The binned scatter's bins for this cfg and batch: returns their number (0:

@@ -1,9 +1,9 @@
 #!/bin/bash
 # A/B: the MLP RAdam step in the backward's slab reduction vs its own launch.
 set -o pipefail
-O=gpurun_out/abm2; mkdir -p $O
+O=gpurun_out/abm3; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 170 --timeout-method thread -k "fused_mlp or fused_table or trainer" > $O/pytest.log 2>&1; RC=$?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 170 --timeout-method thread -k "fused_mlp or fused_table or trainer or dp" > $O/pytest.log 2>&1; RC=$?
 tail -3 $O/pytest.log; [ $RC -eq 0 ] || exit $RC
 for r in 1 2; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --steps 200 > $O/fused_$r.json 2>$O/err || { tail -5 $O/err; exit 1; }

@@ -382,10 +382,12 @@ def test_sample_batch_morton_draws(hn):
 
 def test_trainer_fused_mlp_step_same_trajectory(hn):
     """Trainer.fuse_mlp_step (ABI 13: the ten NeRFSmall RAdam steps applied in
-    the backward's slab reduction, hn_render_bwd_args.mlp_step) against
-    optimizer.step()'s hn_radam_step launch: 8 steps (the first five in
-    RAdam's no-update mode, TV through step 5) leave the table, every weight
-    and every moment bitwise equal."""
+    the backward's slab reduction, hn_render_bwd_args.mlp_step, and the
+    stepped weights repacked for the next forward, which then skips its
+    packing) against optimizer.step()'s hn_radam_step launch and the forward's
+    own packing: 8 steps (the first five in RAdam's no-update mode, TV through
+    step 5; a weight scaled in place after step 6, which must be repacked)
+    leave the table, every weight and every moment bitwise equal."""
     from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
     data = SyntheticBlender(64, 64, 4, DEV, seed=0)
     res = {}
@@ -395,7 +397,10 @@ def test_trainer_fused_mlp_step_same_trajectory(hn):
         tr = Trainer(args, data, DEV, seed=3)
         tr.fuse_mlp_step = fm
         torch.manual_seed(11)
-        losses = [float(tr.step()[0]) for _ in range(8)]
+        losses = [float(tr.step()[0]) for _ in range(6)]
+        with torch.no_grad():
+            tr._ws[3].mul_(0.5)             # the packed copies are stale now
+        losses += [float(tr.step()[0]) for _ in range(2)]
         ws = tr.kw_train["network_fn"].weights() + tr.kw_train["network_fine"].weights()
         st = [tr.optimizer.state[p] for p in ws]
         res[fm] = (losses, tr.embed_fn.table.detach().clone(), [p.detach().clone() for p in ws],
