@@ -1344,13 +1344,15 @@ __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbin
 // no row needs them; a lane whose row does not, absorbs nothing).
 HN_DEV void seg_sum4(float (&v)[4], uint32_t pm, int pp, bool s1, bool s2, bool s4, bool s8) {
   if (!s1) return;
+  // v + (same ? o : 0) as fma(o, same, v): one v_fmac_f32_dpp per value
+  // instead of an add and a select; fma(o, 1, v) rounds like v + o, and
+  // fma(o, 0, v) = v (up to the sign of a zero v, which no record value
+  // carries into the owner's integer sums)
   auto absorb = [&](auto dc, int d) {
     const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
+    const float sf = same ? 1.f : 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float o = dpp_f<decltype(dc)::value>(v[e]);
-      v[e] = same ? v[e] + o : v[e];
-    }
+    for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(dpp_f<decltype(dc)::value>(v[e]), sf, v[e]);
   };
   absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
   if (s2) {
