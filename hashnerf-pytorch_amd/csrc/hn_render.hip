@@ -1337,6 +1337,17 @@ __host__ __device__ inline OvfBook ovf_book(uint32_t* idx, size_t nrec, int nbin
   return o;
 }
 
+// max(|a|, |b|, m) for m >= 0 as one v_max3_f32 with abs modifiers: the
+// compiler's fmaxf in IEEE mode first quiets each input (v_max_f32 x, x), two
+// extra instructions per value.  Plain VALU operands (no MFMA or DPP result
+// read here), so the asm needs no hazard padding; the values are finite (a
+// non-finite one has already set the fault bit).
+HN_DEV float max3_abs(float a, float b, float m) {
+  float r;
+  asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(r) : "v"(a), "v"(b), "v"(m));
+  return r;
+}
+
 // Segmented suffix sum over runs of samples in one voxel along a 16-lane
 // DPP row (the sum of scatter_level_x): lane pp absorbs lane pp + d iff no
 // run head lies in (pp, pp + d]; pm = the row's head mask.  s1..s8:
@@ -1770,7 +1781,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
       v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
       seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
-      vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[c][0]), fabsf(v[c][1]))), fmaxf(fabsf(v[c][2]), fabsf(v[c][3])));
+      vmax = max3_abs(v[c][2], v[c][3], max3_abs(v[c][0], v[c][1], vmax));
     }
     if (mode == kMerged) {
       if (head) {
