@@ -1353,27 +1353,57 @@ HN_DEV float max3_abs(float a, float b, float m) {
 // run head lies in (pp, pp + d]; pm = the row's head mask.  s1..s8:
 // wave-uniform "some run is longer than 1 / 2 / 4 / 8" (steps skipped when
 // no row needs them; a lane whose row does not, absorbs nothing).
-HN_DEV void seg_sum4(float (&v)[4], uint32_t pm, int pp, bool s1, bool s2, bool s4, bool s8) {
-  if (!s1) return;
-  // v + (same ? o : 0) as fma(o, same, v): one v_fmac_f32_dpp per value
-  // instead of an add and a select; fma(o, 1, v) rounds like v + o, and
-  // fma(o, 0, v) = v (up to the sign of a zero v, which no record value
-  // carries into the owner's integer sums)
-  auto absorb = [&](auto dc, int d) {
-    const bool same = pp + d < 16 && ((pm >> (pp + 1)) & ((1u << d) - 1u)) == 0u;
-    const float sf = same ? 1.f : 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(dpp_f<decltype(dc)::value>(v[e]), sf, v[e]);
-  };
-  absorb(std::integral_constant<int, kRowShl<1>>{}, 1);
-  if (s2) {
-    absorb(std::integral_constant<int, kRowShl<2>>{}, 2);
-    if (s4) {
-      absorb(std::integral_constant<int, kRowShl<4>>{}, 4);
-      if (s8) absorb(std::integral_constant<int, kRowShl<8>>{}, 8);
-    }
-  }
+// v + (same ? o : 0) is computed as fma(o, same, v): fma(o, 1, v) rounds
+// like v + o, and fma(o, 0, v) = v (up to the sign of a zero v, which no
+// record value carries into the owner's integer sums).
+// All 4 corner rows of a level at once (the runs, and so `same`, are the
+// rows' common ones), each step 16 v_fmac_f32_dpp: left to the compiler, the
+// fma is packed into v_pk_fma_f32, which cannot take a DPP source, with a
+// v_mov_b32_dpp per value (r05: scatter 0.213 -> 0.202 ms).
+#define HN_SEG_FMAC(C, E, D) \
+  "v_fmac_f32_dpp %[v" #C #E "], %[v" #C #E "], %[sf] row_shl:" #D " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+// The steps as one asm block with wave-uniform branches inside (n = steps
+// to run): the 16 values enter and leave once, without the copies the
+// compiler puts at the joins of separately branched blocks.  Step d's `same`
+// is computed in the block (v_cmp writes vcc, s_nop 1 before the v_cndmask
+// reads it, as the compiler does); its 4 instructions also give the first
+// DPP read its 2 wait states.
+#define HN_SEG_SAME(M)                                                                                       \
+  "v_lshrrev_b32 %[t], %[sh], %[pm]\n"                                                                       \
+  "v_and_b32 %[t], " #M ", %[t]\n"                                                                           \
+  "v_cmp_eq_u32 vcc, 0, %[t]\n"                                                                              \
+  "s_nop 1\n"                                                                                                \
+  "v_cndmask_b32_e64 %[sf], 0, 1.0, vcc\n"
+#define HN_SEG_BODY(D)                                                                                       \
+  HN_SEG_FMAC(0, 0, D) HN_SEG_FMAC(0, 1, D) HN_SEG_FMAC(0, 2, D) HN_SEG_FMAC(0, 3, D) HN_SEG_FMAC(1, 0, D)    \
+  HN_SEG_FMAC(1, 1, D) HN_SEG_FMAC(1, 2, D) HN_SEG_FMAC(1, 3, D) HN_SEG_FMAC(2, 0, D) HN_SEG_FMAC(2, 1, D)    \
+  HN_SEG_FMAC(2, 2, D) HN_SEG_FMAC(2, 3, D) HN_SEG_FMAC(3, 0, D) HN_SEG_FMAC(3, 1, D) HN_SEG_FMAC(3, 2, D)    \
+  HN_SEG_FMAC(3, 3, D)
+HN_DEV void seg_sum16(float (&v)[4][4], uint32_t pm, int pp, bool s1, bool s2, bool s4, bool s8) {
+  // wave-uniform (from ballots); readfirstlane keeps it in an SGPR where the
+  // compiler cannot prove that (the merged-level path)
+  const int n = __builtin_amdgcn_readfirstlane(s1 ? (s2 ? (s4 ? (s8 ? 4 : 3) : 2) : 1) : 0);
+  float t, sf;
+  asm("s_cmp_eq_u32 %[n], 0\n s_cbranch_scc1 Lseg_end%=\n"
+      HN_SEG_SAME(1) HN_SEG_BODY(1)
+      "s_cmp_eq_u32 %[n], 1\n s_cbranch_scc1 Lseg_end%=\n"
+      HN_SEG_SAME(3) HN_SEG_BODY(2)
+      "s_cmp_eq_u32 %[n], 2\n s_cbranch_scc1 Lseg_end%=\n"
+      HN_SEG_SAME(15) HN_SEG_BODY(4)
+      "s_cmp_eq_u32 %[n], 3\n s_cbranch_scc1 Lseg_end%=\n"
+      HN_SEG_SAME(0xff) HN_SEG_BODY(8)
+      "Lseg_end%=:\n"
+      : [v00] "+v"(v[0][0]), [v01] "+v"(v[0][1]), [v02] "+v"(v[0][2]), [v03] "+v"(v[0][3]),
+        [v10] "+v"(v[1][0]), [v11] "+v"(v[1][1]), [v12] "+v"(v[1][2]), [v13] "+v"(v[1][3]),
+        [v20] "+v"(v[2][0]), [v21] "+v"(v[2][1]), [v22] "+v"(v[2][2]), [v23] "+v"(v[2][3]),
+        [v30] "+v"(v[3][0]), [v31] "+v"(v[3][1]), [v32] "+v"(v[3][2]), [v33] "+v"(v[3][3]),
+        [t] "=&v"(t), [sf] "=&v"(sf)
+      : [n] "s"(n), [sh] "v"((uint32_t)pp + 1u), [pm] "v"(pm)
+      : "vcc", "scc");
 }
+#undef HN_SEG_SAME
+#undef HN_SEG_BODY
+#undef HN_SEG_FMAC
 
 // round(v * 2^S) as int64 without f64 arithmetic: x = v * 2^S is exact in fp32
 // (|x| < 2^47, a power-of-2 scale), a = trunc(x / 2^16) is an exact integer
@@ -1765,7 +1795,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     const uint32_t q0 = dpp_u<kRowShr1>(cx), q1 = dpp_u<kRowShr1>(y0), q2 = dpp_u<kRowShr1>(z0);
     bool head = pp == 0 || q0 != cx || q1 != y0 || q2 != z0;
     const uint64_t hb = __ballot(head);
-    const uint32_t pm = (uint32_t)(hb >> (lane & 48)) & 0xffffu;
+    const uint32_t pm = ((uint32_t)(hb >> (lane & 48)) & 0xffffu) | 0x10000u;   // + virtual head 16 (seg_same)
     // lane 0 of every row is a head, so these never carry across rows
     const uint64_t nz1 = ~hb & 0xfffefffefffefffeull, nz2 = nz1 & (nz1 >> 1), nz4 = nz2 & (nz2 >> 2);
     const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
@@ -1780,9 +1810,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const float wy = j ? w[1] : ay;
       const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
       v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
-      seg_sum4(v[c], pm, pp, s1, s2, s4, s8);
-      vmax = max3_abs(v[c][2], v[c][3], max3_abs(v[c][0], v[c][1], vmax));
     }
+    seg_sum16(v, pm, pp, s1, s2, s4, s8);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) vmax = max3_abs(v[c][2], v[c][3], max3_abs(v[c][0], v[c][1], vmax));
     if (mode == kMerged) {
       if (head) {
         // the 4 corner rows' slots: their first probes in flight together (a
