@@ -1801,15 +1801,21 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     const bool s1 = nz1 != 0ull, s2 = nz2 != 0ull, s4 = nz4 != 0ull, s8 = (nz4 & (nz4 >> 4)) != 0ull;
     const float az = 1.f - w[2], ay = 1.f - w[1], ax = 1.f - w[0];
     // d feat / d e_c = ((g * wz) * wy) * wx (trilerp_bwd's order)
-    const float gz[2][2] = {{q.g0 * az, q.g1 * az}, {q.g0 * w[2], q.g1 * w[2]}};   // [k][f]
+    // the two features as one packed pair (v_pk_mul_f32: the same fp32
+    // products, half the instructions; the asm below would otherwise leave
+    // them unpacked)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 g2 = {q.g0, q.g1};
+    const f2 gz[2] = {g2 * az, g2 * w[2]};   // [k] (features f0, f1)
     float vmax = 0.f;   // largest |record value| of the level: the owner's fixed-point scale
     float v[4][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int j = c >> 1, kk = c & 1;
       const float wy = j ? w[1] : ay;
-      const float a0 = gz[kk][0] * wy, a1 = gz[kk][1] * wy;
-      v[c][0] = a0 * ax; v[c][1] = a1 * ax; v[c][2] = a0 * w[0]; v[c][3] = a1 * w[0];
+      const f2 a = gz[kk] * wy;
+      const f2 x0 = a * ax, x1 = a * w[0];
+      v[c][0] = x0.x; v[c][1] = x0.y; v[c][2] = x1.x; v[c][3] = x1.y;
     }
     seg_sum16(v, pm, pp, s1, s2, s4, s8);
 #pragma unroll
