@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round-5 record: GPU tests, smoke, the config-2 line with its CPU baseline and
+# rocprof summary, then configs 3, 4, 5 with rocprof summaries of 3 and 5.
+set -o pipefail
+TAG=${1:-r05z}
+scripts/gpu_check_all.sh $TAG || exit 1
+PROF="3 5" scripts/gpu_bench_all.sh ${TAG}_cfg 3 4 5 || exit 1
