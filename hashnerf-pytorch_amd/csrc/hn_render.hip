@@ -1288,7 +1288,8 @@ HN_DEV size_t rec_wofs(size_t r, size_t nrec) { return 4 * nrec + r; }
 struct BinW {
   float* bins;
   size_t nrec;
-  uint32_t* lcnt;      // LDS [nbins] record counts
+  unsigned long long* lcnt;   // LDS [nbins]: records of the bin (low 32 bits: the slot
+                              // counter), records of it in the current staging phase (high 32)
   uint32_t* lovf;      // LDS: this block's overflow records
   size_t base;         // first record of this block's region of bin 0
   size_t stride;       // records between a block's regions of consecutive bins
@@ -1422,16 +1423,24 @@ HN_DEV long long fx_of(float v, float scale) {
 // record's slot in its bin (LDS counter); rec_store writes it -- split so a
 // caller can have several counter round trips in flight.
 struct RecSlot {
-  uint32_t word, bin, slot;
+  uint32_t word, bin, slot, pj;   // pj: the record's index among the bin's records of the staging phase
 };
-HN_DEV RecSlot rec_slot(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx, uint32_t yy, uint32_t zz) {
+// staged = count the record in the bin's staging-phase half too (one 64-bit
+// LDS add returns both counts: the staging index needs no separate read of
+// the phase's first slot)
+constexpr unsigned long long kCntRec = 1ull, kCntStaged = (1ull << 32) | 1ull;
+HN_DEV RecSlot rec_slot(const BinW& bw, uint32_t l, uint32_t log2T, uint32_t cx, uint32_t yy, uint32_t zz,
+                        unsigned long long inc = kCntRec) {
   const uint32_t mask = (1u << log2T) - 1u;
   const uint32_t flat = (l << log2T) + ((cx ^ yy ^ zz) & mask);
   const uint32_t nbits = (uint32_t)__builtin_ctz(~cx) + 1u;
   RecSlot r;
   r.word = flat | (nbits << 28);
   r.bin = flat >> bw.shift;
-  r.slot = __hip_atomic_fetch_add(bw.lcnt + r.bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const unsigned long long old =
+      __hip_atomic_fetch_add(bw.lcnt + r.bin, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  r.slot = (uint32_t)old;
+  r.pj = (uint32_t)(old >> 32);
   return r;
 }
 HN_DEV void rec_store(const BinW& bw, const RecSlot& rs, const float (&v)[4]) {
@@ -1620,11 +1629,11 @@ static size_t sc_static_lds() {
 // the merge table grows to 4,096 slots only when levels are merged and the
 // whole allocation still fits the CU's LDS
 static int sc_mh_log2(int nbins, int merge_levels) {
-  const size_t cnt = (size_t)((nbins + 3) & ~3) * 4;
+  const size_t cnt = (size_t)((nbins + 3) & ~3) * 8;
   return merge_levels != 0 && sc_static_lds() + cnt + ((size_t)36 << 12) <= kLdsMax ? 12 : 11;
 }
 static size_t sc_lds_bytes(int nbins, int mh_log2) {
-  const size_t cnt = (size_t)((nbins + 3) & ~3) * 4, pool = (size_t)kStPool * 20;
+  const size_t cnt = (size_t)((nbins + 3) & ~3) * 8, pool = (size_t)kStPool * 20;
   const size_t tab = (size_t)36 << mh_log2;
   return cnt + (pool > tab ? pool : tab);
 }
@@ -1651,14 +1660,14 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // dynamic LDS: the bins' record counters, then the staging pool / merge
   // table (sc_lds_bytes)
   extern __shared__ __attribute__((aligned(16))) uint32_t sc_dyn[];
-  uint32_t* const bcnt = sc_dyn;
+  unsigned long long* const bcnt = reinterpret_cast<unsigned long long*>(sc_dyn);   // BinW::lcnt
   __shared__ float gsl[kGsLds], lvmx[16];
   __shared__ uint32_t lovf;
   __shared__ uint32_t lvmxl[16 * 64];
   for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) lvmxl[i] = 0u;
   // wave-uniform work-unit arithmetic (u, ray = u / 3, u % 3, act) on the scalar unit
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = lane_id();
-  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0u;
+  for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) bcnt[i] = 0ull;
   if (threadIdx.x < 16) lvmx[threadIdx.x] = 0.f;
   if (threadIdx.x == 0) lovf = 0u;
   stage_grid_sizes(k.g, gsl);
@@ -1685,7 +1694,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int pp = lane & 15;
   // the staging pool (fine levels) and, over the same LDS, the merge table
   // (merged levels): 80 KiB
-  uint32_t* const st_raw = sc_dyn + ((k.nbins + 3) & ~3);   // 16-B aligned after the counters
+  uint32_t* const st_raw = sc_dyn + 2 * ((k.nbins + 3) & ~3);   // 16-B aligned after the counters
   f32x4* const stv = reinterpret_cast<f32x4*>(st_raw);
   uint32_t* const stw = st_raw + 4 * kStPool;
   const int mh_log2 = k.mh_log2, mh_n = 1 << mh_log2;     // merge table slots
@@ -1700,7 +1709,11 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   int par = 0;
   auto st_init = [&](const StPhase& ph, int pr) {
     if (ph.log2c < kStMinLog2C) return;
-    for (int i = threadIdx.x; i < ph.nbl; i += blockDim.x) stfl[pr][i] = min(bcnt[ph.b0 + i], bw.cap);
+    for (int i = threadIdx.x; i < ph.nbl; i += blockDim.x) {
+      const unsigned long long c = bcnt[ph.b0 + i];
+      stfl[pr][i] = min((uint32_t)c, bw.cap);
+      bcnt[ph.b0 + i] = c & 0xffffffffull;   // the phase's count from 0 (no atomics in flight on it now)
+    }
   };
   // the pool's records of level l to their regions, in slot order
   auto st_flush = [&](const StPhase& ph) {
@@ -1709,7 +1722,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     for (int p = threadIdx.x; p < kStPool; p += blockDim.x) {
       const int bl = p >> ph.log2c, b = ph.b0 + bl;
       const uint32_t j = (uint32_t)p & (c - 1u), f = stfl[par][bl];
-      const uint32_t end = min(min(bcnt[b], bw.cap), f + c);
+      const uint32_t end = min(min((uint32_t)bcnt[b], bw.cap), f + c);
       if (f + j < end) {
         const size_t r = bw.base + (size_t)b * bw.stride + f + j;
         *reinterpret_cast<f32x4*>(bw.bins + rec_vofs(r)) = stv[p];
@@ -1882,11 +1895,14 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {   // 4 counter round trips in flight
         const int j = c >> 1, kk = c & 1;
-        rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)log2T, cx, j ? y0 + kPrimeY : y0, kk ? z0 + kPrimeZ : z0);
+        rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)log2T, cx, j ? y0 + kPrimeY : y0, kk ? z0 + kPrimeZ : z0,
+                         staged ? kCntStaged : kCntRec);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].slot - stfl[par][staged ? bl : 0];
+        // staged index = the record's place among the bin's records of this
+        // phase (its slot minus the phase's first slot whenever slot < cap)
+        const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].pj;
         if (staged && rs[c].slot < bw.cap && j < (1u << ph.log2c)) {
           const int qq = (int)((bl << ph.log2c) + j);
           stv[qq] = f32x4{v[c][0], v[c][1], v[c][2], v[c][3]};
@@ -1955,7 +1971,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
           RecSlot rs;
           rs.word = word;
           rs.bin = (word & 0x0fffffffu) >> bw.shift;
-          rs.slot = __hip_atomic_fetch_add(bw.lcnt + rs.bin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          rs.slot = (uint32_t)__hip_atomic_fetch_add(bw.lcnt + rs.bin, kCntRec, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
           rec_store(bw, rs, v);
         }
         __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
@@ -2037,7 +2054,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   __syncthreads();
   uint32_t* cnt = book + nrec + blockIdx.x;
   for (int i = threadIdx.x; i < k.nbins; i += blockDim.x) {
-    const uint32_t c = bcnt[i];
+    const uint32_t c = (uint32_t)bcnt[i];
     cnt[(size_t)i * kBwdBlocks] = c;
     if (c > bw.cap)   // spilled records of bin i (ovf_place_kernel's bucket sizes)
       __hip_atomic_fetch_add(ob.per_bin + i, c - bw.cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
