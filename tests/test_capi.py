@@ -49,7 +49,8 @@ def test_struct_layouts_match_compiled_header(hn, tmp_path):
                "hn_render_cfg": L.HnRenderCfg, "hn_render_fwd_args": L.HnRenderFwdArgs,
                "hn_render_bwd_args": L.HnRenderBwdArgs, "hn_tv_args": L.HnTvArgs,
                "hn_ray_sampler": L.HnRaySampler, "hn_ray_pool": L.HnRayPool,
-               "hn_radam_tensor": L.HnRadamTensor, "hn_render_loss": L.HnRenderLoss}
+               "hn_radam_tensor": L.HnRadamTensor, "hn_render_loss": L.HnRenderLoss,
+               "hn_uniform_draw": L.HnUniformDraw}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hashnerf_amd.h"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
@@ -98,6 +99,16 @@ def test_argument_validation_without_gpu(hn):
     assert lib.hn_blender_images(x, 1, 5, 4, 1, 1, x, None) == 2
     assert lib.hn_blender_images(x, 1, 4, 4, 0, 3, x, None) == 2
     assert lib.hn_blender_images(None, 0, 4, 4, 1, 1, None, None) == 0
+    # torch.rand restatement (ABI 13): argument checks return before any launch
+    d = (L.HnUniformDraw * 5)()
+    assert lib.hn_uniform_philox(1, d, 5, None) == 2                   # more than HN_UNIFORM_MAX_DRAWS
+    assert lib.hn_uniform_philox(1, None, 1, None) == 1
+    d[0].numel, d[0].threads, d[0].offset = 8, 256, 2                  # offset not a multiple of 4
+    assert lib.hn_uniform_philox(1, d, 1, None) == 2
+    d[0].offset, d[0].out = 4, None
+    assert lib.hn_uniform_philox(1, d, 1, None) == 1                   # no output
+    d[0].numel = 0
+    assert lib.hn_uniform_philox(1, d, 1, None) == 0                   # nothing to draw
 
 
 def test_bins_and_deferred_owner_validation_without_gpu(hn):
