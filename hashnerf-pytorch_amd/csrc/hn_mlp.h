@@ -73,15 +73,62 @@ static_assert(W_END == HN_MLP_PARAMS, "param count");
 
 // acc += A(region R, block ob) . B where bval(s) is the B operand of f32 k-step s.
 // Split-f32: each chunk's A fragments are loaded at use (round 3: loading the
-// next chunk's during the current one's MFMAs measured 0.324 against 0.314 ms
-// for render_fwd_kernel, identical results).  f32: one group ahead.  The
-// scheduling barrier stops hipcc from hoisting all loads (register blowup).
+// next chunk's into registers during the current one's MFMAs measured 0.324
+// against 0.314 ms for render_fwd_kernel, identical results), or, with a
+// FragRing source (the render forward, round 5), read from the wave's LDS slot
+// that a DMA filled during the previous chunk (0.271 -> 0.266 ms, no registers
+// held).  f32: one group ahead.  The scheduling barrier stops hipcc from
+// hoisting all loads (register blowup).
 // Where a GEMM's packed A fragments come from (the packed buffer in global
 // memory: frag_load).
 struct FragGlobal {
+  static constexpr bool kRing = false;
   const float* P;
   HN_DEV f32x4 operator()(int off, int lane) const { return frag_load(P, off, lane); }
 };
+// The forward tile's split-GEMM chunks (3 fragment groups each, contiguous)
+// in the order mlp_fwd_tile_src runs them; a tile's last chunk is followed by
+// the next tile's first.
+struct FwdChunk {
+  int r, ob, c;
+};
+constexpr FwdChunk kFwdSeq[] = {
+    {R_F0, 0, 0}, {R_F0, 0, 1}, {R_F0, 1, 0}, {R_F0, 1, 1}, {R_F1, 0, 0}, {R_F1, 0, 1}, {R_F1, 0, 2},
+    {R_F1, 0, 3}, {R_F2G, 0, 0}, {R_F2G, 1, 0}, {R_F3, 0, 0}, {R_F3, 0, 1}, {R_F3, 0, 2}, {R_F3, 0, 3},
+    {R_F3, 1, 0}, {R_F3, 1, 1}, {R_F3, 1, 2}, {R_F3, 1, 3}, {R_F4, 0, 0}, {R_F4, 0, 1}, {R_F4, 0, 2},
+    {R_F4, 0, 3}};
+constexpr int kFwdSeqN = sizeof(kFwdSeq) / sizeof(kFwdSeq[0]);
+constexpr int fwd_chunk_off(const FwdChunk& q) { return reg_off(q.r) + (q.ob * reg_gpo(q.r) + reg_ns(q.r) * q.c) * 256; }
+// float offset of the chunk after (r, ob, c) in the sequence
+constexpr int fwd_next_off(int r, int ob, int c) {
+  for (int i = 0; i < kFwdSeqN; ++i)
+    if (kFwdSeq[i].r == r && kFwdSeq[i].ob == ob && kFwdSeq[i].c == c) return fwd_chunk_off(kFwdSeq[(i + 1) % kFwdSeqN]);
+  return -1;
+}
+// Split-GEMM fragments prefetched one chunk ahead into this wave's LDS slot
+// (3 x 1 KiB; buffer_load ... lds, no registers held): a chunk's groups are
+// read from the slot, the slot is refilled with the next chunk of kFwdSeq,
+// and that DMA runs under the chunk's split and MFMAs.  fwd_ring_start puts a
+// net's first chunk in the slot before its tiles.
+struct FragRing {
+  static constexpr bool kRing = true;
+  const float* P;
+  float* slot;   // LDS, this wave's 768 floats
+  HN_DEV f32x4 operator()(int off, int lane) const { return frag_load(P, off, lane); }
+};
+HN_DEV void ring_fill(const float* P, float* slot, int off, int lane) {
+  int so = off * 4;
+  asm volatile("" : "+s"(so));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(opaque_ptr(P)), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + 256 * q), 16,
+                                             lane * 16, so + 1024 * q, 0, 0);
+}
+HN_DEV void fwd_ring_start(const float* P, float* slot, int lane) {
+  ring_fill(P, slot, fwd_chunk_off(kFwdSeq[0]), lane);
+}
 template <int R, typename BF, typename Src>
 HN_DEV f32x16 gemm_src(const Src& src, int ob, f32x16 acc, int lane, BF bval);
 template <int R, typename BF>
@@ -97,8 +144,17 @@ HN_DEV f32x16 gemm_src(const Src& src, int ob, f32x16 acc, int lane, BF bval) {
 #pragma unroll
     for (int c = 0; c < KS / 8; ++c) {
       SP<NS> a;
+      if constexpr (Src::kRing && NS == 3) {
+        // this chunk from the slot, then the slot refilled with the next one
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(ld(NS * c + q));
+        for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(*reinterpret_cast<const f32x4*>(src.slot + 256 * q + 4 * lane));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ring_fill(src.P, src.slot, fwd_next_off(R, ob, c), lane);
+      } else {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) a.p[q] = as_bf16x8(ld(NS * c + q));
+      }
       const SP<NS> b = splitn<NS>([&](int j) { return bval(8 * c + j); });
       acc = mfma_split<NS>(a, b, acc);
       __builtin_amdgcn_sched_barrier(0);

@@ -265,6 +265,9 @@ __global__ __launch_bounds__(64 * kFwdBlockWaves)
 __attribute__((amdgpu_waves_per_eu(HN_FWD_WAVES_PER_SIMD, HN_FWD_WAVES_PER_SIMD)))
 void render_fwd_kernel(RenderK k) {
   __shared__ __attribute__((aligned(16))) float smem[kFwdBlockWaves * kFLds + kGsLds];
+  // each wave's split-GEMM fragments one chunk ahead (FragRing, hn_mlp.h):
+  // render_fwd_kernel 0.271 -> 0.266 ms, r05 ring (bitwise-identical outputs)
+  __shared__ __attribute__((aligned(16))) float fring[kFwdBlockWaves][768];
   // the wave index (and with it the ray, its 11 floats and every per-ray
   // address) on the scalar unit: VGPR spills 45 -> 22, render_fwd_kernel
   // 0.296 -> 0.281 ms (r04e)
@@ -321,6 +324,7 @@ void render_fwd_kernel(RenderK k) {
   // ---- coarse network (:540) ----
   c0sh_lds_store(opaque_ptr(k.Pc), sh8, c0l, lane);
   lds_fence_wave();
+  fwd_ring_start(k.Pc, fring[wave], lane);
   for (int tau = 0; tau < kSc / 32; ++tau) {
     const float* P = opaque_ptr(k.Pc);
     const int q = 32 * tau + p;
@@ -334,7 +338,8 @@ void render_fwd_kernel(RenderK k) {
     if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
     MlpAct a;
     f32x16 c2;
-    mlp_fwd_tile_c0<true>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
+    mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
+                           a, c2, lane);
     if (k.feat) store_masks(k.feat, ray, tau, lane, a.m);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
@@ -378,6 +383,8 @@ void render_fwd_kernel(RenderK k) {
   // ---- fine network (:556) ----
   c0sh_lds_store(opaque_ptr(k.Pf), sh8, c0l, lane);   // the coarse tiles' reads are done (in-order LDS)
   lds_fence_wave();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the coarse ring's last (unused) fill has landed
+  fwd_ring_start(k.Pf, fring[wave], lane);
   HN_FT(2);
   for (int tau = 0; tau < kSf / 32; ++tau) {
     const float* P = opaque_ptr(k.Pf);
@@ -411,7 +418,8 @@ void render_fwd_kernel(RenderK k) {
     if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
     MlpAct a;
     f32x16 c2;
-    mlp_fwd_tile_c0<true>(P, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); }, a, c2, lane);
+    mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
+                           a, c2, lane);
     if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
