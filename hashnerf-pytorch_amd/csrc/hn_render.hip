@@ -62,6 +62,7 @@ struct RenderK {
   float *z_coarse, *z_fine, *raw_c, *raw_f;
   uint8_t* fine_src;
   float* feat;    // [B][8 tiles][1024] saved features or NULL
+  int feat_nt;    // saved features stored nontemporally (tables past the MALL)
 };
 
 
@@ -141,11 +142,14 @@ static_assert(kTilesPerRay * (1024 + kMaskWordsPerTile) == HN_RENDER_FEAT_PER_RA
 // activations then differ from the forward's by ~2^-17 relative (the dW
 // operands' own precision), but every ReLU decision is the forward's.
 
-HN_DEV void store_masks(float* __restrict__ base, int64_t ray, int tile, int lane, const uint32_t (&m)[3]) {
+HN_DEV void store_masks(float* __restrict__ base, int64_t ray, int tile, int lane, const uint32_t (&m)[3], bool nt) {
   uint32_t* t = reinterpret_cast<uint32_t*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + kTilesPerRay * 1024) +
                 tile * kMaskWordsPerTile;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) __builtin_nontemporal_store(m[j], t + 64 * j + lane);
+  for (int j = 0; j < 3; ++j) {
+    if (nt) __builtin_nontemporal_store(m[j], t + 64 * j + lane);
+    else t[64 * j + lane] = m[j];
+  }
 }
 HN_DEV void load_masks(const float* __restrict__ base, int64_t ray, int tile, int lane, uint32_t (&m)[3]) {
   const uint32_t* t = reinterpret_cast<const uint32_t*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY +
@@ -153,12 +157,13 @@ HN_DEV void load_masks(const float* __restrict__ base, int64_t ray, int tile, in
 #pragma unroll
   for (int j = 0; j < 3; ++j) m[j] = __builtin_nontemporal_load(t + 64 * j + lane);
 }
-HN_DEV void store_feat(float* __restrict__ base, int64_t ray, int tile, int lane, const f32x16& feat) {
+HN_DEV void store_feat(float* __restrict__ base, int64_t ray, int tile, int lane, const f32x16& feat, bool nt) {
   f32x4* t = reinterpret_cast<f32x4*>(base + (size_t)ray * HN_RENDER_FEAT_PER_RAY + (size_t)tile * 1024);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const f32x4 v = {feat[4 * c], feat[4 * c + 1], feat[4 * c + 2], feat[4 * c + 3]};
-    __builtin_nontemporal_store(v, t + 64 * c + lane);
+    if (nt) __builtin_nontemporal_store(v, t + 64 * c + lane);
+    else t[64 * c + lane] = v;
   }
 }
 
@@ -335,12 +340,12 @@ void render_fwd_kernel(RenderK k) {
     encode_tile(k.g, gsl, k.table, pt, h, feat);
     HN_FWD_PRIO_LO();
     HN_FT_FEAT(0, feat);
-    if (k.feat) store_feat(k.feat, ray, tau, lane, feat);
+    if (k.feat) store_feat(k.feat, ray, tau, lane, feat, k.feat_nt != 0);
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
                            a, c2, lane);
-    if (k.feat) store_masks(k.feat, ray, tau, lane, a.m);
+    if (k.feat) store_masks(k.feat, ray, tau, lane, a.m, k.feat_nt != 0);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -415,12 +420,12 @@ void render_fwd_kernel(RenderK k) {
       }
     }
     HN_FT_FEAT(3, feat);
-    if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat);
+    if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat, k.feat_nt != 0);
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
                            a, c2, lane);
-    if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m);
+    if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m, k.feat_nt != 0);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;
@@ -3149,6 +3154,12 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   k.rgb0 = a->rgb0; k.depth0 = a->depth0; k.acc0 = a->acc0; k.sparsity0 = a->sparsity0;
   k.z_std = a->z_std; k.z_coarse = a->z_coarse; k.z_fine = a->z_fine;
   k.raw_c = a->raw_c; k.raw_f = a->raw_f; k.fine_src = a->fine_src; k.feat = a->feat;
+  // the saved features (32 KB + 6 KB per ray) go through L2 while the table
+  // (16 x 2^T x 8 B) leaves room for them in the 256 MiB MALL, where the
+  // backward finds them (config 2, T=19: forward 260.7 -> 253.6 us, step
+  // -8 us); past it they are streamed (config 3, T=22, cached: forward
+  // 633 -> 682 us)
+  k.feat_nt = cfg->grid.log2_hashmap_size > 20;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdBlockWaves - 1) / kFwdBlockWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdBlockWaves), 0, s, k);
 #if HN_PROFILE
