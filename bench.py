@@ -254,6 +254,46 @@ def optimizer_bytes(tr):
     return total * 4 * 3 * 2
 
 
+# the data-parallel exchange's phases, timed with HIP events on the compute
+# stream (train.ShardedTableStep.step, Trainer.step): reduce-scatter issue to
+# wait, the one hn_radam_step launch (table shard + NeRFSmall tensors), the
+# all-gather, and the NeRFSmall gradients' all-reduce (issued before the
+# reduce-scatter, waited before the step)
+XCHG_TIMERS = ("xchg_reduce_scatter", "xchg_step", "xchg_all_gather", "xchg_mlp_allreduce")
+# DESIGN.md 7's model of the exchange on one MI355X node: ring collectives
+# over xGMI (7 links x ~153 GB/s per GPU, the prompt's figure); each of the
+# reduce-scatter and the all-gather moves (N - 1) / N of the vector per rank.
+# Bounds: one link's bandwidth (a single ring) and all seven.
+XGMI_LINK_GBS = 153.0
+XGMI_LINKS = 7
+
+
+def predicted_exchange_ms(vec_bytes, world):
+    """(one-link, seven-link) lower bounds on reduce-scatter + all-gather (ms)."""
+    b = 2.0 * (world - 1) / world * vec_bytes
+    return (round(b / (XGMI_LINK_GBS * 1e9) * 1e3, 4), round(b / (XGMI_LINKS * XGMI_LINK_GBS * 1e9) * 1e3, 4))
+
+
+def exchange_report(tr, world, mine, worst, backend):
+    """The N > 1 line's exchange fields: the bytes and each phase's time
+    (this rank, and the max over ranks), against DESIGN.md 7's prediction."""
+    x = tr._xchg
+    vec = x.exchange_bytes() if x is not None else None
+    mlp = 4 * sum(p.numel() for p in tr._ws)
+    rep = {"backend": backend, "segments": len(x.segs) if x is not None else None,
+           "exchange_bytes": {"reduce_scatter_in": vec, "all_gather_out": vec, "mlp_allreduce": mlp},
+           "rank0_ms": {k.replace("xchg_", ""): round(v, 4) for k, v in zip(XCHG_TIMERS, mine)},
+           "max_over_ranks_ms": {k.replace("xchg_", ""): round(v, 4) for k, v in zip(XCHG_TIMERS, worst)},
+           "timer": "HIP events on the compute stream around each phase (issue to completion), "
+                    "the same kernel-steps loop as the launch times"}
+    if vec:
+        one, seven = predicted_exchange_ms(vec, world)
+        rep["predicted_rs_plus_ag_ms"] = {"one_link": one, "seven_links": seven,
+                                          "model": f"2 x (N-1)/N x {vec} B over {XGMI_LINK_GBS} GB/s xGMI links"}
+        rep["measured_rs_plus_ag_ms"] = round(worst[0] + worst[2], 4)
+    return rep
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -402,7 +442,7 @@ def main():
     # training loop continuing; the committed rocprofv3 kernel-trace summary of
     # the same command agrees with them (profiles/)
     HF.TIMER.reset()
-    HF.TIMER.names = {"render_fwd", "render_bwd", "render_bwd_owner"}
+    HF.TIMER.names = {"render_fwd", "render_bwd", "render_bwd_owner"} | set(XCHG_TIMERS)
     HF.TIMER.every = 1
     HF.TIMER.enabled = True
     for _ in range(args.kernel_steps):
@@ -411,6 +451,13 @@ def main():
     HF.TIMER.enabled = False
     fwd_ms = HF.TIMER.mean_ms("render_fwd")
     bwd_ms = HF.TIMER.mean_ms("render_bwd") + HF.TIMER.mean_ms("render_bwd_owner")
+    # N > 1: each rank's exchange phases (same timer), then their max over ranks
+    xchg = None
+    if world > 1:
+        xt = torch.tensor([HF.TIMER.mean_ms(k) for k in XCHG_TIMERS], device=dev)
+        xmax = xt.clone()
+        dist.all_reduce(xmax, op=dist.ReduceOp.MAX)
+        xchg = exchange_report(tr, world, xt.tolist(), xmax.tolist(), args.backend)
     # diagnostic, after the timed region: the host's time to enqueue one step
     # (Python + ctypes; the device runs concurrently) -- at or above
     # ms_per_step the host, not the GPU, would set the step rate
@@ -508,6 +555,8 @@ def main():
             line["roofline"].update(atomic_requests=round(atomics), atomic_Greq_per_s=round(rate, 2),
                                     atomic_peak_Greq_per_s=ATOMIC_PEAK_GREQ,
                                     atomic_frac=round(rate / ATOMIC_PEAK_GREQ, 3))
+        if xchg is not None:
+            line["exchange"] = xchg
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, steps=args.cpu_steps)
         print(json.dumps(line), flush=True)

@@ -16,7 +16,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HN_LIB_PATH") or os.path.join(HERE, "lib", "libhashnerf_amd.so")
 MAX_LEVELS = 32
-ABI_VERSION = 13                # HN_ABI_VERSION
+ABI_VERSION = 14                # HN_ABI_VERSION
 RENDER_FEAT_PER_RAY = 9728      # HN_RENDER_FEAT_PER_RAY
 MLP_PARAMS = 9344
 MLP_PACKED_FLOATS = 30208
@@ -42,7 +42,7 @@ class HnMlpGrad(C.Structure):
 class HnRenderCfg(C.Structure):
     _fields_ = [("grid", HnGrid), ("n_samples", C.c_int32), ("n_importance", C.c_int32),
                 ("white_bkgd", C.c_int32), ("lindisp", C.c_int32), ("perturb", C.c_int32),
-                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("merge_levels", C.c_int32)]
+                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("reserved_merge", C.c_int32)]
 
 
 _P = C.c_void_p

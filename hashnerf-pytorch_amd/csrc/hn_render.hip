@@ -1412,8 +1412,7 @@ HN_DEV float max3_abs(float a, float b, float m) {
   HN_SEG_FMAC(2, 2, D) HN_SEG_FMAC(2, 3, D) HN_SEG_FMAC(3, 0, D) HN_SEG_FMAC(3, 1, D) HN_SEG_FMAC(3, 2, D)    \
   HN_SEG_FMAC(3, 3, D)
 HN_DEV void seg_sum16(float (&v)[4][4], uint32_t pm, int pp, bool s1, bool s2, bool s4, bool s8) {
-  // wave-uniform (from ballots); readfirstlane keeps it in an SGPR where the
-  // compiler cannot prove that (the merged-level path)
+  // wave-uniform (from ballots); readfirstlane keeps it in an SGPR
   const int n = __builtin_amdgcn_readfirstlane(s1 ? (s2 ? (s4 ? (s8 ? 4 : 3) : 2) : 1) : 0);
   float t, sf;
   asm("s_cmp_eq_u32 %[n], 0\n s_cbranch_scc1 Lseg_end%=\n"
@@ -1608,8 +1607,6 @@ struct ScK {
   const float* slab;       // NULL: no slab reduction here
   hn_mlp_grad dc, df;
   int32_t overwrite_mlp;
-  int32_t merge_levels;    // levels 0 .. merge_levels-1: records merged per block (merge table)
-  int32_t mh_log2;         // log2 merge-table slots (sc_lds_bytes)
   int32_t has_mstep;       // the NeRFSmall tensors' RAdam steps run in the slab reduction (mstep)
   hn_radam_tensor mstep[10];
 };
@@ -1637,11 +1634,6 @@ constexpr int kBinShift = HN_BIN_SHIFT_DEFAULT;   // preferred log2 entries per 
 // wave cycles), not on the write traffic.
 constexpr int kStLog2 = 12, kStPool = 1 << kStLog2;   // 64 KiB of values + 16 KiB of words
 constexpr int kStMinLog2C = 3;                          // fewer than 8 records per bin: no staging
-// Merge table of the coarse levels (over the pool's LDS, grown to 4,096
-// slots when the bins' counters leave room): entry words and their 4 sums as
-// 64-bit fixed point, 36 B per slot
-constexpr uint32_t kMhEmpty = 0xffffffffu;   // never an entry word (bits 26-27 are zero)
-static_assert((1 << 11) * 36 <= kStPool * 20, "a 2,048-slot merge table fits the staging pool");
 constexpr size_t kLdsMax = 160 * 1024;
 __global__ void scatter_bins_kernel(ScK k);
 // the kernel's static LDS, read once from the code object (a
@@ -1655,17 +1647,9 @@ static size_t sc_static_lds() {
   }
   return v;
 }
-// dynamic LDS of scatter_bins_kernel: the counters, then max(pool, table);
-// the merge table grows to 4,096 slots only when levels are merged and the
-// whole allocation still fits the CU's LDS
-static int sc_mh_log2(int nbins, int merge_levels) {
-  const size_t cnt = (size_t)((nbins + 3) & ~3) * 8;
-  return merge_levels != 0 && sc_static_lds() + cnt + ((size_t)36 << 12) <= kLdsMax ? 12 : 11;
-}
-static size_t sc_lds_bytes(int nbins, int mh_log2) {
-  const size_t cnt = (size_t)((nbins + 3) & ~3) * 8, pool = (size_t)kStPool * 20;
-  const size_t tab = (size_t)36 << mh_log2;
-  return cnt + (pool > tab ? pool : tab);
+// dynamic LDS of scatter_bins_kernel: the bins' counters, then the staging pool
+static size_t sc_lds_bytes(int nbins) {
+  return (size_t)((nbins + 3) & ~3) * 8 + (size_t)kStPool * 20;
 }
 struct StPhase {
   int b0, log2c;   // first bin of the phase's levels, log2 pool records per bin (< kStMinLog2C: direct)
@@ -1687,8 +1671,8 @@ HN_DEV StPhase st_phase(int l, int log2T, int shift, int lg2n = 0) {
 constexpr int kScLpp = 1;
 
 __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
-  // dynamic LDS: the bins' record counters, then the staging pool / merge
-  // table (sc_lds_bytes)
+  // dynamic LDS: the bins' record counters, then the staging pool
+  // (sc_lds_bytes)
   extern __shared__ __attribute__((aligned(16))) uint32_t sc_dyn[];
   unsigned long long* const bcnt = reinterpret_cast<unsigned long long*>(sc_dyn);   // BinW::lcnt
   __shared__ float gsl[kGsLds], lvmx[16];
@@ -1722,18 +1706,12 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   const int64_t u0 = (int64_t)blockIdx.x * per;
   const int64_t u1 = u0 + per < units ? u0 + per : units;
   const int pp = lane & 15;
-  // the staging pool (fine levels) and, over the same LDS, the merge table
-  // (merged levels): 80 KiB
+  // the staging pool: 80 KiB
   uint32_t* const st_raw = sc_dyn + 2 * ((k.nbins + 3) & ~3);   // 16-B aligned after the counters
   f32x4* const stv = reinterpret_cast<f32x4*>(st_raw);
   uint32_t* const stw = st_raw + 4 * kStPool;
-  const int mh_log2 = k.mh_log2, mh_n = 1 << mh_log2;     // merge table slots
-  uint32_t* const mh_w = st_raw;                                                   // [mh_n] words
-  unsigned long long* const mh_v = reinterpret_cast<unsigned long long*>(st_raw + mh_n);   // [4][mh_n]
   __shared__ uint32_t stfl[2][kStPool >> kStMinLog2C];   // per phase parity: first staged slot per bin
-  __shared__ uint32_t mh_bound[16], mh_fail;
   const int log2T = (int)k.g.log2T, sh = k.bin_shift;
-  const int n_merge = k.merge_levels;
   // first staged slot of each bin of level l (the bins' counts so far, capped)
   // (stfl alternates between phases: par = the phase's parity)
   int par = 0;
@@ -1757,14 +1735,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
         const size_t r = bw.base + (size_t)b * bw.stride + f + j;
         rec_put<true>(bw.bins, r, bw.nrec, stv[p], stw[p]);
       }
-    }
-  };
-  // the merge table empty (every merged level leaves it empty again)
-  auto mh_clear = [&]() {
-    for (int s = threadIdx.x; s < mh_n; s += blockDim.x) {
-      mh_w[s] = kMhEmpty;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) mh_v[c * mh_n + s] = 0ull;
     }
   };
   const int64_t n_it = (u1 - u0 + kScWaves - 1) / kScWaves;   // the same for every wave of the block
@@ -1815,21 +1785,13 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     q.g1 = gq.y;
     bad |= !(fabsf(gq.x + gq.y) <= 3.402823466e38f);
   };
-  auto unit_at = [&](int64_t it, int l) {
-    Unit q = unit_base(it);
-    unit_grads(q, l);
-    return q;
-  };
   // The records of one level of a unit: voxel, run heads, per corner row the
   // x-pair sums over runs of samples in one voxel (16-lane rows), then each
-  // head lane's record to sink(c, word, bin-relative slot source, v) per mode:
-  //   kStaged: the staging pool / direct store (slots from the LDS counters),
-  //   kDirect: direct store,
-  //   kMerged: the merge table (int64 at the level's block scale `mscale`)
-  enum { kStaged = 0, kDirect = 1, kMerged = 2 };
-  auto level = [&](const Unit& q, const int l, const int mode, const float mscale, const StPhase& ph) {
+  // head lane's record into the staging pool, or stored directly (slots from
+  // the LDS counters)
+  auto level = [&](const Unit& q, const int l, const StPhase& ph) {
     if (!q.act) return;
-    const bool staged = mode == kStaged && ph.log2c >= kStMinLog2C;
+    const bool staged = ph.log2c >= kStMinLog2C;
     int32_t cell[3];
     float w[3];
     voxel_cw_sc(k.g, gsl, q.pt, q.xc, l, cell, w);
@@ -1862,63 +1824,6 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     seg_sum16(v, pm, pp, s1, s2, s4, s8);
 #pragma unroll
     for (int c = 0; c < 4; ++c) vmax = max3_abs(v[c][2], v[c][3], max3_abs(v[c][0], v[c][1], vmax));
-    if (mode == kMerged) {
-      if (head) {
-        // the 4 corner rows' slots: their first probes in flight together (a
-        // plain read: most inserts find their word already there, and
-        // same-address reads broadcast where compare-and-swaps serialise),
-        // then a claim of the empty ones, then linear probing for the rest
-        uint32_t word[4], s[4], cur[4];
-        bool ok[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int j = c >> 1, kk = c & 1;
-          const uint32_t yy = j ? y0 + kPrimeY : y0, zz = kk ? z0 + kPrimeZ : z0;
-          const uint32_t flat = ((uint32_t)l << log2T) + ((cx ^ yy ^ zz) & ((1u << log2T) - 1u));
-          word[c] = flat | (((uint32_t)__builtin_ctz(~cx) + 1u) << 28);
-          // every value must convert exactly (|v * scale| < 2^46): else the
-          // level is redone unmerged
-          ok[c] = true;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ok[c] = ok[c] && fabsf(v[c][e] * mscale) < 0x1p46f;
-          s[c] = (word[c] * 0x9E3779B1u) >> (32 - mh_log2);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) cur[c] = __hip_atomic_load(mh_w + s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (cur[c] == kMhEmpty) {   // claim it (or find the same word another lane just claimed)
-            __hip_atomic_compare_exchange_strong(mh_w + s[c], &cur[c], word[c], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (cur[c] == kMhEmpty) cur[c] = word[c];
-          }
-        bool fail = false;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          int probes = 1;
-          while (ok[c] && cur[c] != word[c]) {   // linear probing over the whole table: fails only when it is full
-            s[c] = (s[c] + 1u) & (uint32_t)(mh_n - 1);
-            ok[c] = probes++ < mh_n;
-            cur[c] = __hip_atomic_load(mh_w + s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (cur[c] == kMhEmpty) {
-              __hip_atomic_compare_exchange_strong(mh_w + s[c], &cur[c], word[c], __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (cur[c] == kMhEmpty) cur[c] = word[c];
-            }
-          }
-          fail = fail || !ok[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (ok[c])
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              __hip_atomic_fetch_add(mh_v + e * mh_n + s[c], (unsigned long long)fx_of(v[c][e], mscale),
-                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (fail) mh_fail = 1u;
-      }
-      return;   // the flush reports the merged values' maximum
-    }
     RecSlot rs[4];
     if (head) {
 #pragma unroll
@@ -1944,95 +1849,29 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  // Merged levels: the level's scale from a bound on its record values,
-  // 16 x the largest |grad| of the block's units (a run sums <= 16 samples of
-  // one row; trilinear weights are <= 1 inside the box, and a value past the
-  // bound's 2^6 margin sends the level to the unmerged path)
-  if (n_merge > 0) {
-    if (threadIdx.x < 16) mh_bound[threadIdx.x] = 0u;
-    mh_clear();
-    if (threadIdx.x == 0) mh_fail = 0u;
-    __syncthreads();
-    for (int l = 0; l < n_merge; ++l) {
-      float m = 0.f;
-      for (int64_t it = 0; it < n_it; ++it) {
-        const Unit q = unit_at(it, l);
-        m = fmaxf(m, fmaxf(fabsf(q.g0), fabsf(q.g1)));
-      }
-      m = wave_max_f32(m);
-      if (lane == 0)
-        __hip_atomic_fetch_max(mh_bound + l, __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
   // staging phases of 2^lpp levels where each level owns whole bins and the
   // pool still holds >= 2^kStMinLog2C records per bin (T=19: 2 levels per
   // phase, 32 records per bin; T=22: 1 level, 8 per bin)
   const int lg_bins = log2T - sh;   // log2 bins per level
   const int lpp = lg_bins < 0 ? 0 : max(0, min(kScLpp, kStLog2 - kStMinLog2C - lg_bins));
   auto phase_of = [&](int l) { return st_phase(l, log2T, sh, l + (1 << lpp) <= 16 ? lpp : 0); };
-  if (n_merge < 16) st_init(phase_of(n_merge), par);
+  st_init(phase_of(0), par);
   __syncthreads();
-  for (int l = 0; l < n_merge; ++l) {
-    {
-      // scale 2^S: values < 2^(E_B) -> < 2^40 units, E_B the exponent of the bound
-      const float bnd = 16.f * __uint_as_float(mh_bound[l]);
-      const int eb = bnd > 0.f && bnd <= 3.0e38f ? ilogbf(bnd) + 1 : 0;
-      const int S0 = 40 - eb;
-      const int S = S0 > 127 ? 127 : (S0 < -126 ? -126 : S0);
-      const float mscale = ldexpf(1.f, S);
-      for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kMerged, mscale, st_phase(l, log2T, sh));
-      __syncthreads();   // the level's sums are complete
-      const bool failed = mh_fail != 0u;   // uniform
-      if (!failed) {
-        // one record per distinct entry word: the block's exact sum, rounded once to fp32
-        float vmax = 0.f;
-        for (int s = threadIdx.x; s < mh_n; s += blockDim.x) {
-          const uint32_t word = mh_w[s];
-          if (word == kMhEmpty) continue;
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = ldexpf((float)(long long)mh_v[e * mh_n + s], -S);
-            mh_v[e * mh_n + s] = 0ull;
-            vmax = fmaxf(vmax, fabsf(v[e]));
-          }
-          mh_w[s] = kMhEmpty;
-          RecSlot rs;
-          rs.word = word;
-          rs.bin = (word & 0x0fffffffu) >> bw.shift;
-          rs.slot = (uint32_t)__hip_atomic_fetch_add(bw.lcnt + rs.bin, kCntRec, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-          rec_store(bw, rs, v);
-        }
-        __hip_atomic_fetch_max(&lvmxl[l * 64 + lane], __float_as_uint(vmax), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        // the table overflowed (or a value exceeded the bound): this block
-        // writes the level's records unmerged (a function of the block's
-        // records alone, so the result stays deterministic)
-        __syncthreads();   // every lane has read mh_fail
-        mh_clear();
-        if (threadIdx.x == 0) mh_fail = 0u;
-        for (int64_t it = 0; it < n_it; ++it) level(unit_at(it, l), l, kDirect, 1.f, st_phase(l, log2T, sh));
-      }
-      __syncthreads();   // the table is empty again
-    }
-  }
-  // the other levels unit by unit (each unit's ray and rows loaded once),
-  // their records through the staging pool, one phase per (unit round, level)
-  for (int64_t it = 0; it < n_it && n_merge < 16; ++it) {
+  // the levels unit by unit (each unit's ray and rows loaded once), their
+  // records through the staging pool, one phase per (unit round, level group)
+  for (int64_t it = 0; it < n_it; ++it) {
     Unit q = unit_base(it);
-    for (int l = n_merge; l < 16;) {
+    for (int l = 0; l < 16;) {
       const StPhase ph = phase_of(l);
       const int np = l + (1 << lpp) <= 16 ? 1 << lpp : 1;
       for (int j = 0; j < np; ++j, ++l) {
         unit_grads(q, l);
-        level(q, l, kStaged, 1.f, ph);
+        level(q, l, ph);
       }
       __syncthreads();   // the phase's records are in the pool, its counts final
       st_flush(ph);
       // the next phase's bins (other parity), counts unchanged by the flush
-      const int ln = l < 16 ? l : (it + 1 < n_it ? n_merge : 16);
+      const int ln = l < 16 ? l : (it + 1 < n_it ? 0 : 16);
       if (ln < 16) st_init(phase_of(ln), par ^ 1);
       __syncthreads();   // the pool is free again
       par ^= 1;
@@ -2969,6 +2808,7 @@ static int32_t check_cfg(const hn_render_cfg* c) {
   if (c->n_samples != kSc || c->n_importance != kNi) return HN_E_SHAPE;
   if (c->scatter < 0 || c->scatter > 2) return HN_E_SHAPE;
   if (c->bin_cap < 0 || (c->bin_cap & 63)) return HN_E_SHAPE;
+  if (c->reserved_merge != 0) return HN_E_SHAPE;   // reserved (ABI 14: merged coarse-level records removed)
   return HN_OK;
 }
 
@@ -2990,24 +2830,14 @@ struct BinGeom {
 };
 static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   BinGeom g;
-  static const int env_shift = [] {   // HN_BIN_SHIFT: bin size 2^12 or 2^13 entries
-    const char* e = getenv("HN_BIN_SHIFT");
-    const int v = e ? atoi(e) : 0;
-    return v == 12 || v == 13 ? v : kBinShift;
-  }();
-  // 2^12-entry bins (64 KiB of accumulators: two owner workgroups per CU)
-  // unless that needs more bins than the scatter's LDS counters hold
-  const int want = T + 4 - env_shift <= kScMaxBinsLog2 ? env_shift : 13;
+  // 2^12-entry bins (64 KiB of accumulators: two owner workgroups per CU;
+  // compile-time HN_BIN_SHIFT_DEFAULT=12) unless that needs more bins than the
+  // scatter's LDS counters hold
+  const int want = T + 4 - kBinShift <= kScMaxBinsLog2 ? kBinShift : 13;
   g.shift = T + 4 < want ? T + 4 : want;
   g.nbins = 1 << (T + 4 - g.shift);
   const double rpb = (double)((n_rays + kBwdBlocks - 1) / kBwdBlocks);
   const double avg = rpb * (kSf * 4) * ldexp(1.0, g.shift - T);
-  static const int env_cap = [] {   // diagnostic override (HN_BIN_CAP, multiple of 64)
-    const char* e = getenv("HN_BIN_CAP");
-    const int c = e ? atoi(e) : 0;
-    return c > 0 && c % 64 == 0 ? c : 0;
-  }();
-  if (cap_override <= 0) cap_override = env_cap;
   g.cap = cap_override > 0 ? cap_override : (int)(((int64_t)avg + 128 + 63) & ~(int64_t)63);
   // an odd multiple of 64 records: the regions' stride (16 B x cap) then has
   // as few factors of two as the 64-record granule allows.  Measured on
@@ -3019,48 +2849,14 @@ static BinGeom bin_geom(int T, int64_t n_rays, int cap_override) {
   g.floats = nrec * 5 + (size_t)kBwdBlocks * (g.nbins + 16) + ovf_book_words(g.nbins, n_rays) + 4;
   return g;
 }
-// Backward schedule: cfg->scatter 1 = float atomics (fused), 2 = binned
-// (split), 0 = binned unless the environment sets HN_SCATTER=atomic.  The
-// binned scatter keeps per-bin counters in LDS: nbins <= kScMaxBins (T <= 22).
-// Levels whose records the scatter merges per block (a prefix).  The
-// automatic choice (merge_levels = -1) takes the levels of at most
-// kMergeMaxCells cells per axis, where a block's 16 neighbouring rays cross
-// few distinct voxels (config 2: levels 0-9, 2.5-23x fewer records per
-// block, scripts/bin_stats.py --dups).  The default (0) merges none: merged,
-// the owner pass is faster but the table inserts cost more in the scatter
-// (config 2, r04n: scatter + owner 423 us unmerged, 429 / 440 / 442 us with
-// 4 / 7 / 10 levels merged).  HN_SC_MERGE_LEVELS=n sets the default.
-constexpr double kMergeMaxCells = 130.0;
-static int merge_levels(const hn_render_cfg* c) {
-  static const int env = [] {
-    const char* e = getenv("HN_SC_MERGE_LEVELS");
-    return e ? atoi(e) : 0;
-  }();
-  const hn_grid& g = c->grid;
-  const int want = c->merge_levels != 0 ? c->merge_levels : env;
-  if (want >= 0) return want < g.n_levels ? want : g.n_levels;
-  int n = 0;
-  for (int l = 0; l < g.n_levels; ++l) {
-    double cells = 0.0;
-    for (int a = 0; a < 3; ++a) {
-      const double gs = g.grid_size[l][a];
-      const double c = gs > 0.0 ? ((double)g.box_max[a] - g.box_min[a]) / gs : 1e30;
-      cells = c > cells ? c : cells;
-    }
-    if (cells > kMergeMaxCells) break;
-    n = l + 1;
-  }
-  return n;
-}
-
+// Backward schedule: cfg->scatter 1 = float atomics (fused), 2 or 0 = binned
+// (split).  The binned scatter keeps per-bin counters in LDS: nbins <=
+// kScMaxBins (T <= 22); past that, and where a record's two x corners could
+// leave one bin, the float-atomic schedule runs.  (The release library reads
+// no environment: every schedule choice is in hn_render_cfg.)
 static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
-  static int env = -1;
-  if (env < 0) {
-    const char* e = getenv("HN_SCATTER");
-    env = (e && !strcmp(e, "atomic")) ? kModeAtomic : kModeSplit;
-  }
   if (!c) return kModeAtomic;
-  const int want = c->scatter == 1 ? kModeAtomic : c->scatter == 2 ? kModeSplit : env;
+  const int want = c->scatter == 1 ? kModeAtomic : kModeSplit;
   const int T = c->grid.log2_hashmap_size;
   if (want != kModeSplit || (16ll << T) > (long long)kScMaxBins << 13) return kModeAtomic;
   // A record keeps its x1 corner's row as h(x0) ^ (2^nbits - 1), nbits =
@@ -3227,13 +3023,79 @@ extern "C" int32_t hn_render_bwd_owner(const hn_render_cfg* cfg, const hn_render
   return hip_status(hipGetLastError());
 }
 
+// hn_render_bwd with no rays and a TV term (ABI 14): a data-parallel rank that
+// drew no rays still carries the TV term (train.dp_loss puts it on rank 0,
+// run_nerf.py:551-555 / :626-635).  Its gradient goes through the same TV
+// records, overflow placement and exact fixed-point owner pass as a rendering
+// rank's (scatter_bins_kernel with no units and no slab reduction), so it is
+// bitwise reproducible where hn_tv_bwd's float atomics are not.
+static int32_t tv_only_bwd(const hn_render_cfg* cfg, const hn_render_bwd_args* a, void* workspace,
+                           size_t ws_bytes, hipStream_t s) {
+  const int T = cfg->grid.log2_hashmap_size;
+  if (!a->g_tv || (!a->d_table && !a->table_step) || !workspace) return HN_E_NULL;
+  if (a->d_table_mode < 0 || a->d_table_mode > 3 || a->owner_defer || a->mlp_step || a->repack || a->loss)
+    return HN_E_SHAPE;
+  if (bwd_mode(cfg, 0) != kModeSplit) return HN_E_SHAPE;
+  if (a->table_step) {
+    const hn_radam_tensor& ts = *a->table_step;
+    if (ts.n != ((int64_t)16 << T) * 2) return HN_E_SHAPE;
+    if (!ts.p || !ts.m || !ts.v) return HN_E_NULL;
+    if (a->table_live && (a->table_live_levels < 0 || a->table_live_levels > cfg->grid.n_levels || T < 6))
+      return HN_E_SHAPE;
+  }
+  TvK tvk;
+  int nbf, nbb;
+  int32_t st = make_tv(a->tv, tvk, nbf, nbb);
+  if (st) return st;
+  if (a->tv->n_levels != cfg->grid.n_levels || a->tv->log2_hashmap_size != T) return HN_E_SHAPE;
+  for (int l = 0; l < a->tv->n_levels; ++l)
+    if (a->tv->cube[l] > kTvRecMaxCube) return HN_E_SHAPE;
+  if (ws_bytes < hn_render_workspace_bytes(cfg, 0)) return HN_E_WORKSPACE;
+  const BinGeom bg = bin_geom(T, 0, cfg->bin_cap);
+  const size_t sc_lds = sc_lds_bytes(bg.nbins);
+  if (sc_lds + sc_static_lds() > kLdsMax) return HN_E_SHAPE;
+  float* bins = (float*)workspace + ws_layout(cfg, 0, kModeSplit).bins;
+  // the overflow book starts empty (render_comp_bwd_kernel's zero_ovf_book
+  // on a rendering rank): total, per-bin spills, placement cursors
+  const size_t nrec = bin_records(bg.nbins, bg.cap, 0);
+  const OvfBook ob = ovf_book(reinterpret_cast<uint32_t*>(bins + 4 * nrec), nrec, bg.nbins);
+  if ((st = hip_status(hipMemsetAsync(ob.cnt, 0, (1 + 2 * (size_t)bg.nbins) * sizeof(uint32_t), s)))) return st;
+  ScK sk{};
+  sk.g = make_grid_args(cfg->grid);
+  sk.B = 0;
+  sk.bins = bins;
+  sk.bin_cap = bg.cap;
+  sk.bin_shift = bg.shift;
+  sk.nbins = bg.nbins;
+  sk.g_tv = a->g_tv;
+  sk.tv = tvk;
+  int off = 0;
+  for (int l = 0; l < a->tv->n_levels; ++l) {
+    sk.tv_off[l] = off;
+    const int n1 = a->tv->cube[l] + 1;
+    off += (n1 + 1) / 2 * n1 * n1;
+  }
+  for (int l = a->tv->n_levels; l <= 16; ++l) sk.tv_off[l] = off;
+  sk.slab = nullptr;   // no MLP gradients: the caller's stay untouched
+  hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), sc_lds, s, sk);
+  if ((st = hip_status(hipGetLastError()))) return st;
+  hn_render_bwd_args b = *a;
+  b.n_rays = 0;
+  const BinR r = owner_args(cfg, &b, bins, bg, 0);
+  hipLaunchKernelGGL(ovf_place_kernel, dim3(kBwdBlocks), dim3(kPlaceThreads), 0, s, r, PackK{});
+  if ((st = hip_status(hipGetLastError()))) return st;
+  hipLaunchKernelGGL(bin_reduce_kernel, dim3((unsigned)bg.nbins), dim3(kBinThreads),
+                     (size_t)(2 << bg.shift) * sizeof(unsigned long long), s, r);
+  return hip_status(hipGetLastError());
+}
+
 extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_args* a,
                                  void* workspace, size_t ws_bytes, void* stream) {
   int32_t st = check_cfg(cfg);
   if (st) return st;
   if (!a) return HN_E_NULL;
   if (a->n_rays < 0) return HN_E_SHAPE;
-  if (a->n_rays == 0) return HN_OK;
+  if (a->n_rays == 0) return a->tv ? tv_only_bwd(cfg, a, workspace, ws_bytes, (hipStream_t)stream) : HN_OK;
   if (!a->rays || !a->table || !mlp_ok(a->coarse) || !mlp_ok(a->fine)) return HN_E_NULL;
   if (!a->z_coarse || !a->z_fine || !a->raw_c || !a->raw_f || !a->fine_src || !a->feat)
     return HN_E_NULL;
@@ -3326,6 +3188,12 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     }
   }
   const WsLayout wl = ws_layout(cfg, a->n_rays, mode);
+  // the scatter's LDS (bins' counters + staging pool), checked before anything is queued
+  size_t sc_lds = 0;
+  if (mode == kModeSplit) {
+    sc_lds = sc_lds_bytes(bin_geom(T, a->n_rays, cfg->bin_cap).nbins);
+    if (sc_lds + sc_static_lds() > kLdsMax) return HN_E_SHAPE;   // bins beyond the LDS counters' room
+  }
   BinGeom bg{};
   k.bins = nullptr;
   k.bin_cap = k.bin_shift = k.nbins = 0;
@@ -3384,12 +3252,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.dc = a->d_coarse;
     sk.df = a->d_fine;
     sk.overwrite_mlp = (a->d_table_mode & 2) ? 1 : 0;
-    sk.merge_levels = merge_levels(cfg);
-    sk.mh_log2 = sc_mh_log2(sk.nbins, sk.merge_levels);
     sk.has_mstep = a->mlp_step != nullptr;
     for (int t = 0; t < 10; ++t) sk.mstep[t] = sk.has_mstep ? a->mlp_step[t] : hn_radam_tensor{};
-    const size_t sc_lds = sc_lds_bytes(sk.nbins, sk.mh_log2);
-    if (sc_lds + sc_static_lds() > kLdsMax) return HN_E_SHAPE;   // bins beyond the LDS counters' room
     hipLaunchKernelGGL(scatter_bins_kernel, dim3(kBwdBlocks), dim3(64 * kScWaves), sc_lds, s, sk);
     if ((st = hip_status(hipGetLastError()))) return st;
   }

@@ -722,6 +722,36 @@ def tv_bwd(table, mv, cubes, log2T, g_tv, dtable):
                               L.stream(table.device)), "tv_bwd")
 
 
+def tv_bwd_records(cfg, table, mv, cubes, g_tv, d_table, wsb=None):
+    """hn_render_bwd with no rays and a TV term (ABI 14): d_table = sum_l
+    g_tv[l] d tv_l / d table (every entry written) through the binned
+    scatter's TV records and exact owner pass -- bitwise reproducible, where
+    tv_bwd's float atomics are not.  For a data-parallel rank that drew no
+    rays (train.Trainer._empty_rank_grads).  wsb: workspace of >=
+    hn_render_workspace_bytes(cfg, 0) bytes (default a fresh one)."""
+    L.require_device(table, g_tv, d_table)
+    if mv.device != table.device or mv.dtype != torch.int32 or not mv.is_contiguous():
+        raise ValueError("hashnerf_amd.tv_bwd_records: min vertices must be tv_fwd's contiguous device int32 tensor")
+    if not d_table.is_contiguous() or d_table.shape != table.shape:
+        raise ValueError("hashnerf_amd.tv_bwd_records: d_table must be a contiguous tensor shaped like the table")
+    nbytes = L.lib().hn_render_workspace_bytes(cfg, 0)
+    if wsb is None or wsb.numel() * wsb.element_size() < nbytes:
+        wsb = _ws(nbytes, table.device)
+    a = L.HnRenderBwdArgs()
+    a.n_rays = 0
+    tva = _tv_args(table, mv, cubes, cfg.grid.log2_hashmap_size)
+    a.tv = C.cast(C.pointer(tva), C.c_void_p)
+    g = g_tv.contiguous()
+    a.g_tv = g.data_ptr()
+    a.d_table = d_table.data_ptr()
+    a.d_table_mode = 1
+    L.check(L.lib().hn_render_bwd(cfg, a, L.ptr(wsb), wsb.numel() * wsb.element_size(), L.stream(table.device)),
+            "render_bwd (TV only)")
+    if CHECK_FAULTS:
+        L.check_device_faults()
+    return wsb
+
+
 class TVFn(torch.autograd.Function):
     """Per-level hash-table TV (loss.py:11-43) for all levels in one launch."""
 
@@ -770,7 +800,7 @@ def make_render_cfg(grid: L.HnGrid, white_bkgd: bool, lindisp: bool, perturb: bo
                     n_samples: int = 64, n_importance: int = 128, scatter: str = "auto") -> L.HnRenderCfg:
     """hn_render_cfg.  scatter: the backward's table-gradient scatter --
     "binned" (records + exact per-bin owner pass), "atomic" (float atomics),
-    "auto" (binned unless HN_SCATTER=atomic)."""
+    "auto" (binned where the table allows it: T <= 22)."""
     c = L.HnRenderCfg()
     c.grid = grid
     c.n_samples, c.n_importance = n_samples, n_importance

@@ -311,24 +311,38 @@ class ShardedTableStep:
         F_ = self.table.shape[2]
         return buf[self.full:self.full + self.nc].view(-1, F_)
 
+    def exchange_bytes(self):
+        """Bytes each collective of one step moves per rank buffer: the
+        reduce-scatter's input and the all-gather's output (P floats each: the
+        dense tail + the coarse levels' live rows + pad)."""
+        return 4 * self.P
+
     @torch.no_grad()
-    def step(self, coeffs, produce=None):
+    def step(self, coeffs, produce=None, extra=(), pre_step=None):
         """After the backward: exchange the gradient, RAdam step on the shard
         (hn_radam_step, the reference's per-element op forms), all-gather.
         ``produce(k)``: forms segment k's gradient first (the deferred owner
-        pass over seg_bins[k]); None = the gradient is complete."""
+        pass over seg_bins[k]); None = the gradient is complete.  ``extra``:
+        more (p, g, m, v, coeffs) to step in the same hn_radam_step launch
+        (the trainer's NeRFSmall tensors), after ``pre_step()`` (their
+        gradients' all-reduce wait).  bench.py times the reduce-scatter
+        (issue to wait), the step launch and the all-gather on the compute
+        stream (HF.TIMER names xchg_*)."""
         F_ = self.table.shape[2]
         vec_g, vec_p = self.gbuf[self.head:], self.pbuf[self.head:]
         works = []
         last = len(self.segs) - 1
         # (bench.py: the deferred owner pass's launches, bracketed on the compute stream)
         t_own = HF.TIMER.begin("render_bwd_owner") if produce is not None else None
+        t_rs = None
         for k, (lo, hi) in enumerate(self.segs):
             if produce is not None:
                 produce(k)
             if k == last and self.nc:   # the coarse levels' bins are in segment 0's range
                 torch.index_select(self.gbuf[:self.head].view(-1, F_), 0, self.rows, out=self._packed_coarse(self.gbuf))
             o0, o1 = self.shard_offs[k], self.shard_offs[k + 1]
+            if t_rs is None:
+                t_rs = HF.TIMER.begin("xchg_reduce_scatter")
             works.append(self.coll.reduce_scatter(self.g_shard[o0:o1], vec_g[lo:hi], async_op=True))
         HF.TIMER.end("render_bwd_owner", t_own)
         # the shard's parameters (the table may have been loaded since the last step)
@@ -338,7 +352,13 @@ class ShardedTableStep:
         for w in works:
             if w is not None:
                 w.wait()
-        self.stepper([(self.p_shard, self.g_shard, self.m, self.v, coeffs)])
+        HF.TIMER.end("xchg_reduce_scatter", t_rs)
+        if pre_step is not None:
+            pre_step()
+        t_st = HF.TIMER.begin("xchg_step")
+        self.stepper([(self.p_shard, self.g_shard, self.m, self.v, coeffs)] + list(extra))
+        HF.TIMER.end("xchg_step", t_st)
+        t_ag = HF.TIMER.begin("xchg_all_gather")
         if len(self.segs) == 1:   # the shard is one slice of the vector: gathered in place
             self.coll.all_gather(vec_p, self.p_shard)
         else:
@@ -354,6 +374,7 @@ class ShardedTableStep:
                 vec_p[lo:hi].view(self.world, o1 - o0).copy_(g2[:, o0:o1])
         if self.nc:
             self.pbuf[:self.head].view(-1, F_).index_copy_(0, self.rows, self._packed_coarse(self.pbuf))
+        HF.TIMER.end("xchg_all_gather", t_ag)
         self.stale = True
 
     @torch.no_grad()
@@ -582,6 +603,7 @@ class Trainer:
         # ... and then repacks them for the next forward, which reuses the
         # render workspace (kept across steps) instead of packing again
         self._rws = None         # the render workspace
+        self._rws0 = None        # an empty rank's TV-only workspace (before any render)
         self._pk = None          # (workspace, weight versions) its packed copies belong to
         self._pf = None          # (step, batch, ready event) drawn ahead
         # explicit mode: the loss value and its gradients formed by the render
@@ -735,7 +757,10 @@ class Trainer:
         else:
             self._gtable = torch.zeros_like(table)
         self._binned = HF.L.lib().hn_render_scatter_mode(self._cfg, a.N_rand) == 2
+        # the ten MLP gradients: views of ONE flat buffer (the DP exchange
+        # all-reduces it in place, no concatenation or copy-back)
         self._gws = HF.zeros_like_all(self._ws)
+        self._gflat = self._gws[0]._base
         self._one = torch.ones((), device=self.device)
         self._gtv = None
         self._grads = True
@@ -899,10 +924,16 @@ class Trainer:
             tv, mv = HF.tv_fwd(table, mv0, cubes, self.embed_fn.log2_hashmap_size)
             w = self.args.tv_loss_weight
             lo[0] = w * tv.sum()
-            HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, torch.full_like(tv, w), self._gtable)
+            g_tv = torch.full_like(tv, w)
+            if self._binned:
+                # the TV term alone through the binned scatter's records and exact
+                # owner pass (bitwise reproducible, as a rendering rank's TV term)
+                self._rws0 = HF.tv_bwd_records(self._cfg, table, mv, cubes, g_tv, self._gtable,
+                                               wsb=self._rws if self._rws is not None else self._rws0)
+            else:
+                HF.tv_bwd(table, mv, cubes, self.embed_fn.log2_hashmap_size, g_tv, self._gtable)
         table.grad = self._gtable
-        for g in self._gws:
-            g.zero_()
+        self._gflat.zero_()
         for p, g in zip(self._ws, self._gws):
             p.grad = g
         return lo[0], lo[1]
@@ -945,23 +976,27 @@ class Trainer:
             loss.backward()
         if self._xchg is not None and self.mode == "explicit":
             # the table: RAdam state advanced here (take_step), its exchange and
-            # update sharded; the ten MLP gradients all-reduced as one bucket
+            # update sharded; the ten MLP gradients (views of one flat buffer)
+            # all-reduced in place as one bucket beside the table's
+            # reduce-scatter, and their RAdam steps taken in the shard's
+            # hn_radam_step launch (one launch for all eleven tensors)
             table = self.embed_fn.table
             _, _, _, coeffs = self.optimizer.take_step(table)
-            mlp = [p for p in self.grad_vars if p.grad is not None]
-            flat = torch.cat([p.grad.reshape(-1) for p in mlp])
-            work = dist.all_reduce(flat, async_op=True)
+            t_mlp = HF.TIMER.begin("xchg_mlp_allreduce")
+            work = dist.all_reduce(self._gflat, async_op=True)
+            mst = [self.optimizer.take_step(p) for p in self._ws]
+            extra = [(p, g, m, v, c) for (p, m, v, c), g in zip(mst, self._gws)]
+
+            def wait_mlp():
+                work.wait()
+                HF.TIMER.end("xchg_mlp_allreduce", t_mlp)
+
             st, self._owner_st = self._owner_st, None
             produce = None
             if st is not None:
                 sb = self._xchg.seg_bins
                 produce = lambda k: HF.render_bwd_owner(st, *sb[k])
-            self._xchg.step(coeffs, produce=produce)
-            work.wait()
-            off = 0
-            for p in mlp:
-                p.grad.copy_(flat[off:off + p.numel()].view_as(p))
-                off += p.numel()
+            self._xchg.step(coeffs, produce=produce, extra=extra, pre_step=wait_mlp)
             table.grad = None
         else:
             self.allreduce_grads()

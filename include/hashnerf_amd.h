@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 13
+#define HN_ABI_VERSION 14
 #define HN_MAX_LEVELS 32
 
 enum {
@@ -141,18 +141,15 @@ typedef struct hn_render_cfg {
   int32_t white_bkgd;
   int32_t lindisp;
   int32_t perturb;        /* 1: stratified jitter from t_rand */
-  int32_t scatter;        /* backward table-gradient scatter: 0 auto (binned, unless the
-                             environment sets HN_SCATTER=atomic), 1 float atomics,
-                             2 binned (records + exact per-bin owner pass; T <= 22) */
+  int32_t scatter;        /* backward table-gradient scatter: 0 auto (= binned where the
+                             table allows it), 1 float atomics, 2 binned (records +
+                             exact per-bin owner pass; T <= 22).  The library reads no
+                             environment variables (ABI 14). */
   int32_t bin_cap;        /* binned scatter: records per (producer block, bin) region, a
                              multiple of 64; 0 = sized from the batch.  Small values
                              exercise the shared overflow records (tests). */
-  int32_t merge_levels;   /* binned scatter (ABI 12): levels 0..n-1 have their records merged
-                             per producer block before they are stored (one record per
-                             distinct entry word: the block's exact fixed-point sum, rounded
-                             once to fp32); n > 0: levels 0..n-1, -1 = the levels of at most
-                             130 cells per axis, 0 = the default: none (measured slower on
-                             MI355X), or HN_SC_MERGE_LEVELS from the environment */
+  int32_t reserved_merge; /* must be 0 (ABI 14; ABI 12-13's per-block merged coarse-level
+                             records, measured slower on MI355X, were removed) */
 } hn_render_cfg;
 
 #define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the
@@ -240,7 +237,15 @@ typedef struct hn_render_bwd_args {
    * [L] upstream gradients of its per-level values.  With the binned scatter and
    * cubes <= 50 its gradient goes into the bins as records (so table_step stays
    * fused); otherwise it is added to d_table (hn_tv_bwd; table_step not allowed).
-   * NULL = no TV term. */
+   * NULL = no TV term.
+   * ABI 14: n_rays == 0 with a TV term (a data-parallel rank that drew no rays,
+   * run_nerf.py:551-555, still carries the TV term) runs the TV term alone through
+   * the same records and exact owner pass -- bitwise reproducible, unlike
+   * hn_tv_bwd's float atomics; only cfg, tv, g_tv, d_table (or table_step),
+   * d_table_mode and the workspace (hn_render_workspace_bytes(cfg, 0)) are read,
+   * the MLP gradients are not touched, owner_defer must be 0.  The binned scatter
+   * is required (else HN_E_SHAPE: use hn_tv_bwd).  n_rays == 0 without a TV term
+   * does nothing. */
   const struct hn_tv_args* tv;
   const float* g_tv;
   /* Optional with table_step (ABI 11): the live row pairs of the table's leading
@@ -423,8 +428,8 @@ int32_t hn_loss_fwd_bwd(const float* rgb, const float* rgb0, const float* target
 
 size_t hn_render_workspace_bytes(const hn_render_cfg* cfg, int64_t n_rays);
 /* The table-gradient scatter hn_render_bwd runs for this configuration and
- * batch (1 float atomics, 2 binned), after cfg->scatter, HN_SCATTER, the
- * table size and the record buffer size. */
+ * batch (1 float atomics, 2 binned), after cfg->scatter, the table size and
+ * the box's cell counts. */
 int32_t hn_render_scatter_mode(const hn_render_cfg* cfg, int64_t n_rays);
 int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_args* a,
                       void* workspace, size_t ws_bytes, void* stream);

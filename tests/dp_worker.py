@@ -103,8 +103,8 @@ def train_pool(out_path, steps, emulate, tv=True):
     # 1 image of 7 x 19 = 133 rays = 2 x 66 + 1: every second step's batch is
     # 1 ray (rank 0 draws none, rank 1 the one: train._pool_draw's split)
     data = SyntheticBlender(7, 19, 1, dev, seed=0)
-    # (tv=False: the empty rank's TV backward is the float-atomic hn_tv_bwd,
-    # whose sums are not bitwise reproducible; comparisons run without TV)
+    # (the empty rank's TV term goes through the binned records: bitwise
+    # reproducible, so the comparisons run with it)
     args = default_args(N_rand=66, log2_hashmap_size=14, tv_loss_weight=1e-4 if tv else 0.0, tv_until=10 ** 6,
                         sparse_loss_weight=1e-3, no_batching=False)
     tr = Trainer(args, data, dev, rank=rank, world=world, seed=0)

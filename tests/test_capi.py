@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(hn):
     for n in names:
         assert hasattr(lib, n), n
         assert n in hn._lib.SIGNATURES, f"ctypes signature missing for {n}"
-    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 13
+    assert lib.hn_abi_version() == hn._lib.ABI_VERSION == 14
 
 
 def test_struct_sizes_match_header(hn):
@@ -144,6 +144,43 @@ def test_bins_and_deferred_owner_validation_without_gpu(hn):
     assert lib.hn_render_bwd_owner(cfg, a, x, ws, 0, 1025, None) == 2          # past the last bin
     assert lib.hn_render_bwd_owner(cfg, a, x, ws, 7, 3, None) == 2             # reversed range
     assert lib.hn_render_bwd_owner(cfg, a, x, ws, 5, 5, None) == 0             # empty range: no-op
+
+
+def test_zero_ray_backward_validation_without_gpu(hn):
+    """ABI 14: hn_render_bwd with n_rays == 0 is a no-op without a TV term;
+    with one it is the TV-only records path, which checks its arguments
+    before any launch (needs g_tv and d_table, the binned scatter, no owner
+    deferral); the reserved field of hn_render_cfg must be 0."""
+    L = hn._lib
+    lib = L.lib()
+    HF = hn.functional
+    box = (torch.tensor([-1.5, -1.5, -1.5]), torch.tensor([1.5, 1.5, 1.5]))
+    emb = hn.HashEmbedder(box, log2_hashmap_size=19, finest_resolution=512)
+    cfg = HF.make_render_cfg(emb.grid(), True, False, True, scatter="binned")
+    x = C.c_void_p(16)   # never dereferenced: validation happens before any launch
+    a = L.HnRenderBwdArgs()
+    a.n_rays = 0
+    assert lib.hn_render_bwd(cfg, a, None, 0, None) == 0                        # nothing to do
+    tva = L.HnTvArgs()
+    tva.n_levels, tva.log2_hashmap_size = 16, 19
+    for l in range(16):
+        tva.cube[l] = 8
+    tva.min_vertex = tva.table = 16
+    a.tv = C.cast(C.pointer(tva), C.c_void_p)
+    ws = lib.hn_render_workspace_bytes(cfg, 0)
+    assert lib.hn_render_bwd(cfg, a, x, ws, None) == 1                          # no g_tv / d_table
+    a.g_tv, a.d_table, a.d_table_mode = 16, 16, 1
+    assert lib.hn_render_bwd(cfg, a, x, ws - 4, None) == 3                      # workspace too small
+    a.owner_defer = 1
+    assert lib.hn_render_bwd(cfg, a, x, ws, None) == 2                          # no deferred owner here
+    a.owner_defer = 0
+    tva.cube[3] = 51
+    assert lib.hn_render_bwd(cfg, a, x, ws, None) == 2                          # cube past the records' bound
+    tva.cube[3] = 8
+    cfg_a = HF.make_render_cfg(emb.grid(), True, False, True, scatter="atomic")
+    assert lib.hn_render_bwd(cfg_a, a, x, ws, None) == 2                        # float-atomic schedule: hn_tv_bwd
+    cfg.reserved_merge = 4
+    assert lib.hn_render_bwd(cfg, a, x, ws, None) == 2                          # reserved field set
 
 
 def test_product_path_refuses_cpu_tensors(hn):

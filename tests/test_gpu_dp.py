@@ -122,9 +122,11 @@ def test_dp_device_collectives_production_calls(hn, tmp_path):
     """The sharded exchange on device tensors through the production calls
     (reduce_scatter_tensor with async_op, all_gather_into_tensor) on gloo,
     against the emulation the GPU tests use by default: the same table after
-    six steps (incl. the empty-rank steps above, TV off: the empty rank's TV
-    backward is the float-atomic hn_tv_bwd, not bitwise reproducible; with
-    it the two runs' tables differed, r05a-d).  First a probe of the two
+    six steps, incl. the empty-rank steps above with the TV term on the empty
+    rank (round 6: its TV gradient goes through the binned records and the
+    exact owner pass, hn_render_bwd with n_rays = 0, instead of the
+    float-atomic hn_tv_bwd whose sums made the two runs' tables differ,
+    r05a-d).  First a probe of the two
     calls on small device tensors: where this gloo build does not give their
     defined results for device tensors the comparison is skipped with the
     probe's numbers -- the production calls are then pinned by the CPU gloo
@@ -139,7 +141,7 @@ def test_dp_device_collectives_production_calls(hn, tmp_path):
     res = {}
     for em in ("1", "0"):
         out = str(tmp_path / f"pool_{em}.pt")
-        _launch(["train_pool", out, "6", em, "0"])
+        _launch(["train_pool", out, "6", em, "1"])
         res[em] = torch.load(out, weights_only=True)
     assert torch.equal(res["0"]["table"], res["1"]["table"])
 

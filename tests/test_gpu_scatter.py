@@ -142,30 +142,6 @@ def test_binned_overflow_records(hn):
     assert _rel(t_small, t_full) <= 1e-6, _rel(t_small, t_full)
 
 
-@pytest.mark.parametrize("box", ["chair", "clumped"])
-def test_merged_levels_match_unmerged(hn, box):
-    """hn_render_cfg.merge_levels (0 = none, the default; -1 = automatic;
-    n = levels 0..n-1): the coarse levels' records merged per
-    producer block (one record per distinct entry word, the block's exact
-    fixed-point sum rounded once) against every record stored: the same
-    gradient to fp32 rounding, each form bitwise reproducible.  16 merged
-    levels overflow the block's merge table on the fine levels (or exceed the
-    scale bound outside the clumped box), which then fall back to unmerged
-    records."""
-    bx = BOX if box == "chair" else (torch.tensor([-1.0, -1.0, -1.0]), torch.tensor([1.0, 1.0, 1.0]))
-    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 4096, 19, 11, "binned", box=bx)
-    out = {}
-    for n in (0, -1, 4, 16):
-        st.cfg.merge_levels = n
-        t1, _ = _bwd(HF, emb, ws, st, grads)
-        t2, _ = _bwd(HF, emb, ws, st, grads)
-        assert torch.equal(t1, t2), f"merge_levels={n}: table gradient changed between identical launches"
-        out[n] = t1
-    assert torch.count_nonzero(out[0]) > 0
-    for n in (-1, 4, 16):
-        assert _rel(out[n], out[0]) <= 1e-6, (n, _rel(out[n], out[0]))
-
-
 def test_binned_clumped_box(hn):
     """scannet-style box (bench config 5): samples mostly outside the box,
     the regions of the surface voxels' bins spill; binned == atomic."""
@@ -421,6 +397,39 @@ def test_tv_records_match_tv_bwd(hn):
     assert _rel(d_b, d_a) <= 1e-6, _rel(d_b, d_a)
     # TV-only difference resolved too (the render part cancels exactly: integer sums)
     assert _rel(d_b - _bwd(HF, emb, ws, st, grads)[0], tv_only) <= 1e-5
+
+
+@pytest.mark.parametrize("T", [14, 19])
+def test_tv_only_records_bitwise(hn, T):
+    """hn_render_bwd with no rays and a TV term (ABI 14; a data-parallel rank
+    that drew no rays, train.Trainer._empty_rank_grads): the TV gradient
+    through the records and the exact owner pass equals hn_tv_bwd's float
+    atomics (loss.py:11-43) to fp32 summation order, writes every entry
+    (d_table_mode 1: a NaN-filled buffer comes back finite), is bitwise
+    repeatable, and leaves the render workspace's packed weights alone."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 256, T, 29, "binned")
+    mvd, cubes, g_tv = _tv_inputs(HF, emb, seed=7)
+    table = emb.table.detach()
+    d_a = torch.zeros_like(table)
+    HF.tv_bwd(table, mvd, cubes, emb.log2_hashmap_size, g_tv, d_a)
+    packed = st.wsb[:4 * 2 * 30208].clone()
+    outs = []
+    for _ in range(2):
+        d_b = torch.full_like(table, float("nan"))
+        HF.tv_bwd_records(st.cfg, table, mvd, cubes, g_tv, d_b, wsb=st.wsb)
+        torch.cuda.synchronize()
+        HF.L.check_device_faults()
+        outs.append(d_b)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.count_nonzero(d_a) > 0
+    assert _rel(outs[0], d_a) <= 1e-6, _rel(outs[0], d_a)
+    assert torch.equal(st.wsb[:4 * 2 * 30208], packed)
+    # a fresh workspace of hn_render_workspace_bytes(cfg, 0) gives the same bits
+    d_c = torch.full_like(table, float("nan"))
+    HF.tv_bwd_records(st.cfg, table, mvd, cubes, g_tv, d_c)
+    torch.cuda.synchronize()
+    assert torch.equal(d_c, outs[0])
 
 
 @pytest.mark.parametrize("mode", [1, 2])
