@@ -702,8 +702,14 @@ struct WRing {
 
 // Weight-fragment group load: frag_load (hn_common.h, raw buffer load with a
 // scalar offset).
+// HN_DIAG_FRAG_L1 (diagnostic builds only, wrong gradients): every group
+// load reads the same 1 KiB, so the stream is served from the CU's L1 --
+// the bound on what sharing the fragments between waves could save.
+#ifndef HN_DIAG_FRAG_L1
+#define HN_DIAG_FRAG_L1 0
+#endif
 HN_DEV f32x4 wload(const float* P, int off, int lane) {
-  return frag_load(P, off, lane);
+  return frag_load(P, HN_DIAG_FRAG_L1 ? 0 : off, lane);
 }
 
 // (offsets are constexpr-evaluated: left to the optimiser, the region

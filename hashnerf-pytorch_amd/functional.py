@@ -603,11 +603,15 @@ _SAMPLER_WS = {}
 
 
 def _sampler_ws(dev, nbytes):
-    """Per-device scratch of the Morton sampler (block counts), grown on demand."""
-    ws = _SAMPLER_WS.get(dev)
+    """Scratch of the Morton sampler (block counts), grown on demand: one per
+    (device, stream), so a batch drawn ahead on a side stream
+    (Trainer.prefetch) never shares it with a draw on the current stream
+    (ADVICE r05)."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0)
+    ws = _SAMPLER_WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _SAMPLER_WS[dev] = ws
+        _SAMPLER_WS[key] = ws
     return ws
 
 

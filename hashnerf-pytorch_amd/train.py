@@ -756,6 +756,7 @@ class Trainer:
             self._gtable = self._xchg.grad_view()
         else:
             self._gtable = torch.zeros_like(table)
+        self._pk = None          # (re)setup: the weights may have been replaced
         self._binned = HF.L.lib().hn_render_scatter_mode(self._cfg, a.N_rand) == 2
         # the ten MLP gradients: views of ONE flat buffer (the DP exchange
         # all-reduces it in place, no concatenation or copy-back)
@@ -905,8 +906,16 @@ class Trainer:
     def _pack_key(self):
         """What the workspace's packed weights must match: the buffer and
         every weight's version counter (an in-place change of a weight, e.g.
-        a checkpoint load, bumps it; the HIP optimizer's writes do not)."""
+        a checkpoint load, bumps it; the HIP optimizer's writes do not).  A
+        write the version counter does not see (``p.data = ...``,
+        ``p.data.copy_``, a raw-pointer write) must call invalidate_packed()."""
         return (self._rws.data_ptr(), tuple(p._version for p in self._ws))
+
+    def invalidate_packed(self):
+        """Forget the render workspace's packed MLP copies: the next forward
+        packs the weights again.  Call after changing a NeRFSmall weight in a
+        way its version counter does not record."""
+        self._pk = None
 
     def _empty_rank_grads(self, batch):
         """A rank that drew no rays this step (world > 1, use_batching: the
