@@ -348,6 +348,9 @@ def main():
                     help="A/B: the loss in its own hn_loss_fwd_bwd launch instead of the backward's pre-pass")
     ap.add_argument("--separate-mlp-step", action="store_true",
                     help="A/B: the MLP RAdam step in its own hn_radam_step launch")
+    ap.add_argument("--dense-bwd", action="store_true",
+                    help="A/B: the backward also computes the samples whose d raw is exactly zero "
+                         "(hn_render_cfg.dense_bwd; the default skips them, same results)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only for rehearsals)")
     args = ap.parse_args()
@@ -413,6 +416,7 @@ def main():
     tr.prefetch = args.prefetch
     tr.fuse_loss = not args.separate_loss
     tr.fuse_mlp_step = not args.separate_mlp_step
+    tr.dense_bwd = args.dense_bwd
 
     for _ in range(args.pretrain):
         tr.step()                             # reference loop index global_step + 1

@@ -42,7 +42,7 @@ class HnMlpGrad(C.Structure):
 class HnRenderCfg(C.Structure):
     _fields_ = [("grid", HnGrid), ("n_samples", C.c_int32), ("n_importance", C.c_int32),
                 ("white_bkgd", C.c_int32), ("lindisp", C.c_int32), ("perturb", C.c_int32),
-                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("reserved_merge", C.c_int32)]
+                ("scatter", C.c_int32), ("bin_cap", C.c_int32), ("dense_bwd", C.c_int32)]
 
 
 _P = C.c_void_p

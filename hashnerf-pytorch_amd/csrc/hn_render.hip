@@ -96,6 +96,8 @@ struct B1K {
   int32_t n_tv;
   float lgm, lsparse, lworld, lsparse_w, ltv_w;
   float* lout;
+  int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
+  uint8_t* uflags;      // [B][2] per (ray, pass): bit u = unit u has a nonzero d raw (composite pre-pass)
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -1263,6 +1265,14 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
   lds_fence_wave();
 }
 
+// Samples with d raw = 0 (relu(sigma) = 0) have no gradient at all: the MLP
+// backward skips their units and the scatter their feature grads and zero
+// records (b1_unit_split, scatter_bins_kernel), unless hn_render_cfg.dense_bwd
+// asks for every sample to be computed (B1K / ScK skip_zero = 0).
+HN_DEV bool draw_nonzero(const float4& d) {
+  return ((__float_as_uint(d.x) | __float_as_uint(d.y) | __float_as_uint(d.z) | __float_as_uint(d.w)) << 1) != 0u;
+}
+
 // ---- binned table-gradient scatter (HN_SCATTER=split) ----------------------
 // The memory-side float-atomic rate (~20 G requests/s, one per 64-B segment
 // of a wave-instruction) bounds the atomic scatter.  The binned scatter sends
@@ -1600,6 +1610,9 @@ struct ScK {
   const uint8_t* fine_src;
   const float* dfeat_f;   // [B][6][1024] tile order (split render_bwd_kernel)
   const float* dfeat_c;   // [B][2][1024] tile order (coarse units of the split render_bwd_kernel)
+  const float* draw;      // [B][64 + 192][4] d raw (composite pre-pass): zero = no feature grads to read
+  int32_t scramble;       // the MLP backward's ray permutation (B1K::scramble; 0: identity)
+  int32_t skip_zero;      // exact-zero skipping (!hn_render_cfg.dense_bwd)
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
@@ -1749,11 +1762,23 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     bool act;
     Ray r;
     float pt[3], xc[3];
-    const float* tb;   // the sample's fine grads (tile order)
-    const float* tw;   // its coarse twin's grads, or null
+    const float* tb;   // the sample's fine grads (tile order), or null: exactly zero
+    const float* tw;   // its coarse twin's grads, or null (none, or exactly zero)
     float g0, g1;      // the current level's two feature grads (fine + coarse twin)
   };
   bool bad = false;   // a non-finite grad or point seen by this lane
+  // the MLP backward's ray order (render_bwd_kernel's block_ray): block b's
+  // units are the rays MLP block b processed, spread over the batch, so the
+  // units without any gradient (below) spread evenly over the blocks
+  auto unit_ray = [&](int64_t j) -> int64_t {
+    uint32_t x = (uint32_t)j;
+    if (k.scramble) {
+      do {
+        x = feistel(x, k.scramble, 0x5bd1e995u);
+      } while ((int64_t)x >= k.B);
+    }
+    return (int64_t)x;
+  };
   // unit u0 + wave + it * kScWaves: its ray, the lane's sample point and grad rows
   auto unit_base = [&](int64_t it) {
     Unit q;
@@ -1762,16 +1787,24 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     q.g0 = q.g1 = 0.f;
     q.tb = q.tw = nullptr;
     if (q.act) {
-      const int64_t ray = u / 3;
+      const int64_t ray = unit_ray(u / 3);
       const int i = 64 * (int)(u % 3) + lane;       // fine sample
       load_ray(k.rays, ray, q.r);
       ray_point(q.r, k.z_fine[ray * kSf + i], q.pt);
 #pragma unroll
       for (int a = 0; a < 3; ++a) q.xc[a] = clamp_t(q.pt[a], k.g.bmin[a], k.g.bmax[a]);
-      q.tb = k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024 + 4 * (i & 31);
-      const int src = k.fine_src[ray * kSf + i];
-      if (src < kSc) q.tw = k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024 + 4 * (src & 31);
       bad |= !(fabsf((q.pt[0] + q.pt[1]) + q.pt[2]) <= 3.402823466e38f);
+      // a sample whose d raw is exactly zero has exactly zero feature grads (the
+      // MLP backward did not store them: b1_unit_split's skip); the same for
+      // its coarse twin
+      const float* dr = k.draw + (size_t)ray * (kSc + kSf) * 4;
+      if (!k.skip_zero || draw_nonzero(*reinterpret_cast<const float4*>(dr + 4 * (kSc + i))))
+        q.tb = k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024 + 4 * (i & 31);
+      const int src = k.fine_src[ray * kSf + i];
+      if (src < kSc && (!k.skip_zero || draw_nonzero(*reinterpret_cast<const float4*>(dr + 4 * src))))
+        q.tw = k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024 + 4 * (src & 31);
+      // no lane with a gradient: the unit writes no record (wave-uniform)
+      q.act = __ballot(q.tb != nullptr || q.tw != nullptr) != 0ull;
     }
     return q;
   };
@@ -1782,7 +1815,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   auto unit_grads = [&](Unit& q, int l) {
     if (!q.act) return;
     const int lp = l >> 1, o = 4 * (64 * (lp >> 1) + 32 * (lp & 1)) + 2 * (l & 1);
-    float2 gq = *reinterpret_cast<const float2*>(q.tb + o);
+    float2 gq = q.tb ? *reinterpret_cast<const float2*>(q.tb + o) : make_float2(0.f, 0.f);
     if (q.tw) {
       const float2 t = *reinterpret_cast<const float2*>(q.tw + o);
       gq = make_float2(gq.x + t.x, gq.y + t.y);
@@ -1831,15 +1864,25 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) vmax = max3_abs(v[c][2], v[c][3], max3_abs(v[c][0], v[c][1], vmax));
     RecSlot rs[4];
+    // a run whose four sums are exactly zero (samples without gradient, or a
+    // zero trilinear weight) adds nothing to the owner's integer sums: no
+    // record (the same table gradient bitwise; not with dense_bwd)
+    bool put[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      put[c] = head && (!k.skip_zero || ((__float_as_uint(v[c][0]) | __float_as_uint(v[c][1]) |
+                                           __float_as_uint(v[c][2]) | __float_as_uint(v[c][3])) << 1) != 0u);
     if (head) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {   // 4 counter round trips in flight
         const int j = c >> 1, kk = c & 1;
-        rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)log2T, cx, j ? y0 + kPrimeY : y0, kk ? z0 + kPrimeZ : z0,
-                         staged ? kCntStaged : kCntRec);
+        if (put[c])
+          rs[c] = rec_slot(bw, (uint32_t)l, (uint32_t)log2T, cx, j ? y0 + kPrimeY : y0, kk ? z0 + kPrimeZ : z0,
+                           staged ? kCntStaged : kCntRec);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
+        if (!put[c]) continue;
         // staged index = the record's place among the bin's records of this
         // phase (its slot minus the phase's first slot whenever slot < cap)
         const uint32_t bl = rs[c].bin - (uint32_t)ph.b0, j = rs[c].pj;
@@ -2184,16 +2227,30 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 // unit templates): 87 KB of code -> ~25 KB, under the 64 KB instruction cache
 // two CUs share (wave 0 ran the coarse copies, waves 1-3 the fine ones, at
 // the same time).
+// A unit (two tiles) whose 64 samples all have d raw = 0 (raw2outputs'
+// backward gives exactly that to every sample with relu(sigma) = 0: alpha =
+// 0, weight 0, run_nerf_helpers.py:577-628) has an exactly zero MLP
+// backward: zero feature grads, and it adds 0 to every dW accumulator.  Such
+// units are skipped -- the same results bitwise (an accumulator plus exact
+// zeros is unchanged) for ~2/3 of the units of a trained scene (config 2:
+// 57 % of the coarse and 70 % of the fine tiles, scripts/zero_grad_frac.py).
+// Nothing is stored for them: the scatter kernel reads a sample's feature
+// grads only where its own d raw (or its coarse twin's) is nonzero.  The
+// weight ring is aligned to the tile period, so a skipped unit leaves it
+// ready for the next one.  The composite pre-pass marks the units with a
+// nonzero d raw (B1K::uflags), and each wave iterates over the set bits of a
+// ballot of its units' marks: the same loop shape as over every unit (a
+// per-unit test inside the loop made the register allocator spill).
 HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float* X, DW& dw, WRing& wr) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
-  Ray r;
-  load_ray(k.rays, ray, r);
   const int tile0 = 2 * part;
   const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
   float4 dr[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(drs + 128 * t);
+  Ray r;
+  load_ray(k.rays, ray, r);
   float sh8[8], shx8[8];
   ray_sh(r, h, sh8, shx8);
   {
@@ -2319,8 +2376,13 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   else
     composite_bwd<kSc / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
   lds_fence_wave();
-  for (int j = lane; j < S; j += 64)
-    *reinterpret_cast<float4*>(dst + 4 * j) = *reinterpret_cast<const float4*>(rawb + 4 * j);
+  uint32_t nzu = 0u;   // bit u: a sample of MLP unit u (64 samples) has a nonzero d raw
+  for (int j = lane; j < S; j += 64) {
+    const float4 d = *reinterpret_cast<const float4*>(rawb + 4 * j);
+    *reinterpret_cast<float4*>(dst + 4 * j) = d;
+    nzu |= (__ballot(draw_nonzero(d)) != 0ull ? 1u : 0u) << (j >> 6);
+  }
+  if (lane == 0) k.uflags[2 * ray + (fine ? 1 : 0)] = (uint8_t)nzu;
 }
 
 // acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS),
@@ -2446,7 +2508,13 @@ void render_bwd_kernel(B1K k) {
     const bool fine = wv != 0;
     const int part = fine ? wv - 1 : 0;
     wring_prime(wr, fine ? k.Pf : k.Pc, lane);
-    for (int i = 0; i < n_rays; ++i) b1_unit_split(k, block_ray(i), part, fine, X, dw, wr);
+    // the units with a nonzero d raw, 64 at a time (the others add exact zeros)
+    for (int c0 = 0; c0 < n_rays; c0 += 64) {
+      const int i = c0 + lane;
+      const bool nz = i < n_rays && (!k.skip_zero || ((k.uflags[2 * block_ray(i) + (fine ? 1 : 0)] >> part) & 1u));
+      for (uint64_t m = __ballot(nz); m != 0ull; m &= m - 1ull)
+        b1_unit_split(k, block_ray(c0 + (int)__builtin_ctzll(m)), part, fine, X, dw, wr);
+    }
     dw_flush<true>(dw, k.slab + ((size_t)blockIdx.x * kSlabSlots + wv) * W_END, lane);
   } else {
     if (wave == 0) {
@@ -2814,7 +2882,7 @@ static int32_t check_cfg(const hn_render_cfg* c) {
   if (c->n_samples != kSc || c->n_importance != kNi) return HN_E_SHAPE;
   if (c->scatter < 0 || c->scatter > 2) return HN_E_SHAPE;
   if (c->bin_cap < 0 || (c->bin_cap & 63)) return HN_E_SHAPE;
-  if (c->reserved_merge != 0) return HN_E_SHAPE;   // reserved (ABI 14: merged coarse-level records removed)
+  if (c->dense_bwd < 0 || c->dense_bwd > 1) return HN_E_SHAPE;
   return HN_OK;
 }
 
@@ -2886,7 +2954,7 @@ static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   return kModeSplit;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
-// coarse-pass feature grads [n][64][32] | d raw [n][256][4] | split: fine
+// coarse-pass feature grads [n][64][32] | d raw [n][256][4] | unit marks [n][2] u8 (padded) | split: fine
 // feature grads [n][6][1024] and the records (bin_geom).
 struct WsLayout {
   size_t dfeat_f, bins, total;
@@ -2894,7 +2962,8 @@ struct WsLayout {
 static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
-  w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4;
+  w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4 +
+              ((n + 3) & ~(size_t)3);   // + the unit marks, 2 bytes per ray (B1K::uflags)
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -3115,6 +3184,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   float* slab = Pf + G_END;
   float* dfeat = slab + (size_t)kBwdBlocks * kSlabSlots * W_END;
   float* draw = dfeat + (size_t)a->n_rays * kDcRay;
+  uint8_t* uflags = reinterpret_cast<uint8_t*>(draw + (size_t)a->n_rays * (kSc + kSf) * 4);
   if (!a->weights_packed && (st = mlp_pack2_launch(&a->coarse, Pc, &a->fine, Pf, s))) return st;
   B1K k;
   k.B = a->n_rays;
@@ -3135,10 +3205,12 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.slab = slab;
   k.dfeat = dfeat;
   k.draw = draw;
+  k.uflags = uflags;
   k.ltarget = k.lrgb = k.lrgb0 = k.lsp = k.lsp0 = k.ltv = nullptr;
   k.n_tv = 0;
   k.lgm = k.lsparse = k.lworld = k.lsparse_w = k.ltv_w = 0.f;
   k.lout = nullptr;
+  k.skip_zero = cfg->dense_bwd ? 0 : 1;
   if (a->loss) {   // ABI 13: the training loss formed by the pre-pass (hn_render_loss)
     const hn_render_loss& L = *a->loss;
     if (!L.target || !L.rgb || !L.rgb0 || !L.sparsity || !L.sparsity0 || !L.out || (L.n_tv && !L.tv))
@@ -3234,6 +3306,9 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.g = k.g;
     sk.B = a->n_rays;
     sk.rays = a->rays;
+    sk.draw = draw;
+    sk.scramble = k.scramble;
+    sk.skip_zero = k.skip_zero;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
     sk.dfeat_f = k.dfeat_f;

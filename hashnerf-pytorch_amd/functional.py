@@ -801,15 +801,20 @@ SCATTER_MODES = {"auto": 0, "atomic": 1, "binned": 2}
 
 
 def make_render_cfg(grid: L.HnGrid, white_bkgd: bool, lindisp: bool, perturb: bool,
-                    n_samples: int = 64, n_importance: int = 128, scatter: str = "auto") -> L.HnRenderCfg:
+                    n_samples: int = 64, n_importance: int = 128, scatter: str = "auto",
+                    dense_bwd: bool = False) -> L.HnRenderCfg:
     """hn_render_cfg.  scatter: the backward's table-gradient scatter --
     "binned" (records + exact per-bin owner pass), "atomic" (float atomics),
-    "auto" (binned where the table allows it: T <= 22)."""
+    "auto" (binned where the table allows it: T <= 22).  dense_bwd: compute
+    the backward of every sample, also those whose d raw is exactly zero
+    (relu(sigma) = 0), which the default skips (ABI 14; same results up to
+    the sign of zero)."""
     c = L.HnRenderCfg()
     c.grid = grid
     c.n_samples, c.n_importance = n_samples, n_importance
     c.white_bkgd, c.lindisp, c.perturb = int(white_bkgd), int(lindisp), int(perturb)
     c.scatter = SCATTER_MODES[scatter]
+    c.dense_bwd = int(bool(dense_bwd))
     return c
 
 

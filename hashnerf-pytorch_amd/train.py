@@ -611,6 +611,11 @@ class Trainer:
         # launch
         self.fuse_loss = True
         self._side = None
+        # the backward skips the samples whose d raw is exactly zero (relu(sigma)
+        # = 0: no gradient at all; hn_render_cfg.dense_bwd, ABI 14): True
+        # computes them too (A/B: bench.py --dense-bwd; same results up to the
+        # sign of zero)
+        self.dense_bwd = False
 
     def _train_image(self):
         """np.random.choice(i_train) (run_nerf.py:578) from the host generator."""
@@ -733,7 +738,8 @@ class Trainer:
             raise NotImplementedError("Trainer(mode='explicit') needs the HashNeRF configuration")
         a = self.args
         self._cfg = HF.make_render_cfg(self.embed_fn.grid(), bool(kw.get("white_bkgd", False)),
-                                       bool(kw.get("lindisp", False)), kw.get("perturb", 0.) > 0.)
+                                       bool(kw.get("lindisp", False)), kw.get("perturb", 0.) > 0.,
+                                       dense_bwd=self.dense_bwd)
         self._t_vals = _linspace_cached(kw["N_samples"], self.device)
         self._ws = nf.weights() + nfine.weights()
         table = self.embed_fn.table

@@ -148,8 +148,11 @@ typedef struct hn_render_cfg {
   int32_t bin_cap;        /* binned scatter: records per (producer block, bin) region, a
                              multiple of 64; 0 = sized from the batch.  Small values
                              exercise the shared overflow records (tests). */
-  int32_t reserved_merge; /* must be 0 (ABI 14; ABI 12-13's per-block merged coarse-level
-                             records, measured slower on MI355X, were removed) */
+  int32_t dense_bwd;      /* ABI 14 (in ABI 12-13's merge_levels slot, whose merged coarse-level
+                             records were removed): 0 = the backward skips the samples whose
+                             d raw is exactly zero (relu(sigma) = 0: alpha = 0, weight 0), whose
+                             feature and weight gradients are exactly zero -- the same results
+                             up to the sign of zero; 1 = every sample computed (A/B, tests) */
 } hn_render_cfg;
 
 #define HN_RENDER_FEAT_PER_RAY 9728   /* (64 + 192) points x 16 levels x 2 features, then the

@@ -150,7 +150,7 @@ def test_zero_ray_backward_validation_without_gpu(hn):
     """ABI 14: hn_render_bwd with n_rays == 0 is a no-op without a TV term;
     with one it is the TV-only records path, which checks its arguments
     before any launch (needs g_tv and d_table, the binned scatter, no owner
-    deferral); the reserved field of hn_render_cfg must be 0."""
+    deferral); hn_render_cfg.dense_bwd must be 0 or 1."""
     L = hn._lib
     lib = L.lib()
     HF = hn.functional
@@ -179,8 +179,8 @@ def test_zero_ray_backward_validation_without_gpu(hn):
     tva.cube[3] = 8
     cfg_a = HF.make_render_cfg(emb.grid(), True, False, True, scatter="atomic")
     assert lib.hn_render_bwd(cfg_a, a, x, ws, None) == 2                        # float-atomic schedule: hn_tv_bwd
-    cfg.reserved_merge = 4
-    assert lib.hn_render_bwd(cfg, a, x, ws, None) == 2                          # reserved field set
+    cfg.dense_bwd = 4
+    assert lib.hn_render_bwd(cfg, a, x, ws, None) == 2                          # dense_bwd is 0 or 1
 
 
 def test_product_path_refuses_cpu_tensors(hn):
