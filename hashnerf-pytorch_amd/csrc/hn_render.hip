@@ -98,6 +98,7 @@ struct B1K {
   float* lout;
   int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
   uint8_t* uflags;      // [B][2] per (ray, pass): bit u = unit u has a nonzero d raw (composite pre-pass)
+  int32_t* gsplit;      // split schedule: the waves g < *gsplit ran coarse units (slab_reduce_block)
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -1545,16 +1546,21 @@ constexpr int kSlabIlp = 8;   // slab loads in flight per thread (a power of 2)
 // with its final gradient (radam_kernel's update) where that is formed.
 HN_DEV void slab_reduce_block(const float* __restrict__ slab, int n_blocks, const hn_mlp_grad& dc,
                               const hn_mlp_grad& df, int overwrite, int vblock, float (*part)[64],
-                              const hn_radam_tensor* ms = nullptr) {
+                              const hn_radam_tensor* ms = nullptr, const int32_t* gsplit = nullptr) {
   const int lane = threadIdx.x & 63;
   const int e = vblock * 64 + lane;
   const int grp = threadIdx.x >> 6;
   const bool fine = e >= W_END;
   const int i = fine ? e - W_END : e;
-  // the slabs summed for this element: (block, slot) pairs, slot 0 (coarse)
-  // or 1..3 (fine), flattened
-  const int per = fine ? kSlabSlots - 1 : 1, n_slabs = n_blocks * per;
+  // the slabs summed for this element.  gsplit (the split schedule's balanced
+  // unit lists): one slab per MLP wave g = wave * n_blocks + block, waves
+  // g < *gsplit coarse, the others fine; otherwise (block, slot) pairs, slot
+  // 0 (coarse) or 1..3 (fine), flattened
+  const int gs = gsplit ? *gsplit : 0;
+  const int per = fine ? kSlabSlots - 1 : 1;
+  const int n_slabs = gsplit ? (fine ? kSlabSlots * n_blocks - gs : gs) : n_blocks * per;
   auto slab_at = [&](int q) {
+    if (gsplit) return slab[(size_t)(fine ? gs + q : q) * W_END + i];
     const int b = q / per, slot = fine ? 1 + q % per : 0;
     return slab[((size_t)b * kSlabSlots + slot) * W_END + i];
   };
@@ -1613,6 +1619,7 @@ struct ScK {
   const float* draw;      // [B][64 + 192][4] d raw (composite pre-pass): zero = no feature grads to read
   int32_t scramble;       // the MLP backward's ray permutation (B1K::scramble; 0: identity)
   int32_t skip_zero;      // exact-zero skipping (!hn_render_cfg.dense_bwd)
+  const int32_t* gsplit;  // the MLP backward's coarse / fine wave split (slab_reduce_block)
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
@@ -1770,7 +1777,22 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   // the MLP backward's ray order (render_bwd_kernel's block_ray): block b's
   // units are the rays MLP block b processed, spread over the batch, so the
   // units without any gradient (below) spread evenly over the blocks
+#ifndef HN_SC_CHUNK
+#define HN_SC_CHUNK 1
+#endif
   auto unit_ray = [&](int64_t j) -> int64_t {
+    if (HN_SC_CHUNK == 0) return j;
+    if (HN_SC_CHUNK > 1 && k.B % HN_SC_CHUNK == 0 && k.B >= 4 * HN_SC_CHUNK) {
+      // chunks of HN_SC_CHUNK consecutive (Morton-neighbour) rays, the chunks
+      // permuted over the batch
+      int bits = 2;
+      while ((1ll << bits) < k.B / HN_SC_CHUNK) bits += 2;
+      uint32_t c = (uint32_t)(j / HN_SC_CHUNK);
+      do {
+        c = feistel(c, bits / 2, 0x5bd1e995u);
+      } while ((int64_t)c >= k.B / HN_SC_CHUNK);
+      return (int64_t)c * HN_SC_CHUNK + j % HN_SC_CHUNK;
+    }
     uint32_t x = (uint32_t)j;
     if (k.scramble) {
       do {
@@ -1997,7 +2019,8 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       __syncthreads();
       const int vb = vb_sh;
       if (vb >= kSlabVBlocks) break;
-      slab_reduce_block(k.slab, kBwdBlocks, k.dc, k.df, k.overwrite_mlp, vb, part, k.has_mstep ? k.mstep : nullptr);
+      slab_reduce_block(k.slab, kBwdBlocks, k.dc, k.df, k.overwrite_mlp, vb, part, k.has_mstep ? k.mstep : nullptr,
+                        k.gsplit);
     }
   }
 }
@@ -2500,22 +2523,104 @@ void render_bwd_kernel(B1K k) {
   if (wave == kMW && !SPLIT) {
     ring_drain<CAP>(k, ring, V, 2 * kSf / 64 * n_rays);
   } else if (SPLIT) {
-    // split: wave 0 the block's coarse units (slab slot 0), waves 1-3 part
-    // wave - 1 of every ray's fine units (slots 1-3) -- a static split, so each
-    // dW slab, and with the fixed-order slab reduce the MLP gradients, are
-    // bitwise reproducible
-    const int wv = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform (SGPR) pass and part
-    const bool fine = wv != 0;
-    const int part = fine ? wv - 1 : 0;
-    wring_prime(wr, fine ? k.Pf : k.Pc, lane);
-    // the units with a nonzero d raw, 64 at a time (the others add exact zeros)
-    for (int c0 = 0; c0 < n_rays; c0 += 64) {
-      const int i = c0 + lane;
-      const bool nz = i < n_rays && (!k.skip_zero || ((k.uflags[2 * block_ray(i) + (fine ? 1 : 0)] >> part) & 1u));
-      for (uint64_t m = __ballot(nz); m != 0ull; m &= m - 1ull)
-        b1_unit_split(k, block_ray(c0 + (int)__builtin_ctzll(m)), part, fine, X, dw, wr);
+    // Balanced unit lists (round 6).  The units with a nonzero d raw (the
+    // composite pre-pass's marks; all of them with dense_bwd) form two lists in
+    // ray order -- coarse units, then fine units (ray, part) -- and the
+    // kB1Waves x nb MLP waves g = wave * nb + block split them: the first
+    // gsplit waves the coarse list, the others the fine list, in contiguous
+    // slices of equal length (gsplit in proportion to the two lists).  Every
+    // wave then runs ~1/1024 of the work, whatever the scene leaves nonzero;
+    // each wave keeps one net's dW and stores it to slab g, which the scatter
+    // kernel's slab reduction sums in g order: deterministic (the split is a
+    // function of the marks alone).  Every block computes the same prefix sums
+    // over the marks and materializes its 4 waves' slices in LDS (V), in
+    // rounds of kUlCap units (one round unless a wave has more).
+    constexpr int kUlCap = kVoxF / kB1Waves;                 // unit codes per wave and round
+    int* ul = reinterpret_cast<int*>(V);
+    int* scn = reinterpret_cast<int*>(slots);                // [2][kB1Waves] wave totals
+    const int nthr = 64 * kB1Waves, t = threadIdx.x;
+    const int64_t R = (k.B + nthr - 1) / nthr, ra = (int64_t)t * R, rb = ra + R < k.B ? ra + R : k.B;
+    auto cmark = [&](int64_t r) -> int { return k.skip_zero ? (int)(k.uflags[2 * r] & 1u) : 1; };
+    auto fmark = [&](int64_t r) -> uint32_t { return k.skip_zero ? (uint32_t)(k.uflags[2 * r + 1] & 7u) : 7u; };
+    int sc = 0, sf = 0;
+    for (int64_t r = ra; r < rb; ++r) {
+      sc += cmark(r);
+      sf += __builtin_popcount(fmark(r));
     }
-    dw_flush<true>(dw, k.slab + ((size_t)blockIdx.x * kSlabSlots + wv) * W_END, lane);
+    const int ic = (int)wave_incl_sum((double)sc), jf = (int)wave_incl_sum((double)sf);
+    if (lane == 63) {
+      scn[wave] = ic;
+      scn[kB1Waves + wave] = jf;
+    }
+    __syncthreads();
+    int64_t pc = ic - sc, pf = jf - sf;   // this thread's first list positions
+    int nc = 0, nf = 0;                   // the list lengths (made wave-uniform below)
+    for (int q = 0; q < kB1Waves; ++q) {
+      if (q < wave) {
+        pc += scn[q];
+        pf += scn[kB1Waves + q];
+      }
+      nc += scn[q];
+      nf += scn[kB1Waves + q];
+    }
+    const int64_t Nc = __builtin_amdgcn_readfirstlane(nc), Nf = __builtin_amdgcn_readfirstlane(nf);
+    const int G = kB1Waves * (int)nb;
+    int gc = Nc > 0 ? G : 0;                                 // waves on the coarse list
+    if (Nc > 0 && Nf > 0) {
+      gc = (int)((2 * (int64_t)G * Nc + Nc + Nf) / (2 * (Nc + Nf)));
+      gc = gc < 1 ? 1 : (gc > G - 1 ? G - 1 : gc);
+    }
+    if (blockIdx.x == 0 && t == 0) *k.gsplit = gc;
+    int64_t wlo[kB1Waves], whi[kB1Waves];
+    int rounds = 0;
+#pragma unroll
+    for (int w = 0; w < kB1Waves; ++w) {
+      const int g = w * (int)nb + (int)blockIdx.x;
+      const bool fw = g >= gc;
+      const int64_t N = fw ? Nf : Nc;
+      const int gi = fw ? g - gc : g, GG = fw ? G - gc : gc;
+      wlo[w] = GG ? (int64_t)gi * N / GG : 0;
+      whi[w] = GG ? (int64_t)(gi + 1) * N / GG : 0;
+      const int nr = (int)((whi[w] - wlo[w] + kUlCap - 1) / kUlCap);
+      rounds = nr > rounds ? nr : rounds;
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(wave);    // wave-uniform (SGPR)
+    const int g_me = wv * (int)nb + (int)blockIdx.x;
+    const bool fine = g_me >= gc;                            // wave-uniform
+    wring_prime(wr, fine ? k.Pf : k.Pc, lane);
+    for (int rd = 0; rd < rounds; ++rd) {
+      // this round's window of each wave's slice: the codes (ray << 3 | fine << 2 | part)
+      int64_t xc = pc, xf = pf;
+      for (int64_t r = ra; r < rb; ++r) {
+        const int cm = cmark(r);
+        const uint32_t fm = fmark(r);
+#pragma unroll
+        for (int w = 0; w < kB1Waves; ++w) {
+          const bool fw = w * (int)nb + (int)blockIdx.x >= gc;
+          const int64_t a = wlo[w] + (int64_t)rd * kUlCap, e = whi[w] < a + kUlCap ? whi[w] : a + kUlCap;
+          if (!fw && cm && xc >= a && xc < e) ul[w * kUlCap + (int)(xc - a)] = (int)(r << 3);
+          if (fw) {
+            int64_t y = xf;
+            for (int part = 0; part < 3; ++part)
+              if ((fm >> part) & 1u) {
+                if (y >= a && y < e) ul[w * kUlCap + (int)(y - a)] = (int)(r << 3) | 4 | part;
+                ++y;
+              }
+          }
+        }
+        xc += cm;
+        xf += __builtin_popcount(fm);
+      }
+      __syncthreads();
+      const int64_t a = wlo[wv] + (int64_t)rd * kUlCap;
+      const int n = __builtin_amdgcn_readfirstlane((int)((whi[wv] < a + kUlCap ? whi[wv] : a + kUlCap) - a));
+      for (int j = 0; j < n; ++j) {
+        const int code = __builtin_amdgcn_readfirstlane(ul[wv * kUlCap + j]);
+        b1_unit_split(k, (int64_t)(code >> 3), code & 3, fine, X, dw, wr);
+      }
+      if (rd + 1 < rounds) __syncthreads();   // the list is rewritten next round
+    }
+    dw_flush<true>(dw, k.slab + (size_t)g_me * W_END, lane);
   } else {
     if (wave == 0) {
       wring_prime(wr, k.Pc, lane);
@@ -3206,6 +3311,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.dfeat = dfeat;
   k.draw = draw;
   k.uflags = uflags;
+  // the split schedule's coarse / fine wave split, after the marks (2 bytes per ray)
+  k.gsplit = reinterpret_cast<int32_t*>(uflags + ((2 * (size_t)a->n_rays + 3) & ~(size_t)3));
   k.ltarget = k.lrgb = k.lrgb0 = k.lsp = k.lsp0 = k.ltv = nullptr;
   k.n_tv = 0;
   k.lgm = k.lsparse = k.lworld = k.lsparse_w = k.ltv_w = 0.f;
@@ -3309,6 +3416,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.draw = draw;
     sk.scramble = k.scramble;
     sk.skip_zero = k.skip_zero;
+    sk.gsplit = k.gsplit;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
     sk.dfeat_f = k.dfeat_f;

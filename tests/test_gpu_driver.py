@@ -424,8 +424,11 @@ def test_zero_gradient_skip_bitwise(hn):
     1000 training steps on the procedural chair (empty space learned: most
     samples have sigma <= 0) the table gradient and the ten NeRFSmall
     gradients of one batch equal those of the dense backward bitwise, up to
-    the sign of zero (x + 0.0 normalises -0.0), and a large share of the
-    units was skipped."""
+    the sign of zero (x + 0.0 normalises -0.0) for the table (exact integer
+    sums), and within 1e-5 for the NeRFSmall gradients (the MLP backward's
+    balanced unit lists give the two forms different per-wave groupings of the
+    same products); each form is bitwise repeatable, and a large share of
+    the units was skipped."""
     from hashnerf_pytorch_amd import functional as HF
     from hashnerf_pytorch_amd.train import SyntheticBlender, Trainer, default_args
     # bench.py's configs[1] workload (400 x 400, 100 views, T=19, 4096 rays)
@@ -452,6 +455,8 @@ def test_zero_gradient_skip_bitwise(hn):
     assert skipped > 0.3, f"only {skipped:.2f} of the fine units have no gradient"
     dense, sk, sk2 = out[1][0], out[0][0], out[0][1]
     assert torch.count_nonzero(dense[0]) > 0
+    assert torch.equal(dense[0], sk[0]), "table gradient: skipping changed it"
     for k, (a, b, c) in enumerate(zip(dense, sk, sk2)):
-        assert torch.equal(a, b), f"gradient {k}: skipping changed it"
+        rel = float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+        assert rel <= 1e-5, f"gradient {k}: skipped vs dense relative {rel:.3e}"
         assert torch.equal(b, c), f"gradient {k}: not repeatable"
