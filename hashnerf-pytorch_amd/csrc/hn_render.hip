@@ -97,7 +97,8 @@ struct B1K {
   float lgm, lsparse, lworld, lsparse_w, ltv_w;
   float* lout;
   int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
-  uint8_t* uflags;      // [B][2] per (ray, pass): bit u = unit u has a nonzero d raw (composite pre-pass)
+  uint8_t* uflags;      // [B][kMarkB] unit marks (composite pre-pass): [0] coarse, [1] fine MLP units with a
+                        // nonzero d raw, [2] fine units with a nonzero sample or coarse twin (the scatter's)
   int32_t* gsplit;      // split schedule: the waves g < *gsplit ran coarse units (slab_reduce_block)
 };
 
@@ -1266,6 +1267,7 @@ HN_DEV void fill_slot(float* S, const Ray& r, float z, const f32x16& dfeat, cons
   lds_fence_wave();
 }
 
+constexpr int kMarkB = 4;   // unit-mark bytes per ray (B1K::uflags)
 // Samples with d raw = 0 (relu(sigma) = 0) have no gradient at all: the MLP
 // backward skips their units and the scatter their feature grads and zero
 // records (b1_unit_split, scatter_bins_kernel), unless hn_render_cfg.dense_bwd
@@ -1620,6 +1622,7 @@ struct ScK {
   int32_t scramble;       // the MLP backward's ray permutation (B1K::scramble; 0: identity)
   int32_t skip_zero;      // exact-zero skipping (!hn_render_cfg.dense_bwd)
   const int32_t* gsplit;  // the MLP backward's coarse / fine wave split (slab_reduce_block)
+  const uint8_t* uflags;  // [B][kMarkB] unit marks (byte 2: fine units with feature grads), or null
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
@@ -1727,10 +1730,47 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
 
   bw.cap = (uint32_t)k.bin_cap;
   bw.shift = (uint32_t)k.bin_shift;
-  const int64_t units = 3 * k.B;
-  const int64_t per = (units + gridDim.x - 1) / gridDim.x;
-  const int64_t u0 = (int64_t)blockIdx.x * per;
-  const int64_t u1 = u0 + per < units ? u0 + per : units;
+  // The block's units.  With exact-zero skipping: its slice of the list of
+  // fine units that have feature grads to scatter (the composite pre-pass's
+  // marks, byte 2), the list in ray order and cut into equal slices over the
+  // blocks -- every block the same share of the work, whatever the scene
+  // leaves nonzero; every block computes the same prefix over the marks.
+  // Otherwise (dense_bwd, or more than kScListCap units per block) every unit,
+  // the rays permuted as the MLP backward's (unit_ray).
+  constexpr int kScListCap = 256;
+  __shared__ int slist[kScListCap];
+  __shared__ int sc_tot[kScWaves];
+  const bool use_list = k.skip_zero && k.uflags != nullptr && 3 * k.B <= (int64_t)kScListCap * gridDim.x;
+  int64_t u0 = 0, u1 = 0;
+  if (use_list) {
+    const int64_t R = (k.B + blockDim.x - 1) / blockDim.x, ra = (int64_t)threadIdx.x * R;
+    const int64_t rb = ra + R < k.B ? ra + R : k.B;
+    int cnt = 0;
+    for (int64_t r = ra; r < rb; ++r) cnt += __builtin_popcount(k.uflags[kMarkB * r + 2] & 7u);
+    const int inc = (int)wave_incl_sum((double)cnt);
+    if (lane == 63) sc_tot[wave] = inc;
+    __syncthreads();
+    int64_t x = inc - cnt, N = 0;
+    for (int q = 0; q < kScWaves; ++q) {
+      if (q < wave) x += sc_tot[q];
+      N += sc_tot[q];
+    }
+    const int64_t s0 = (int64_t)blockIdx.x * N / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * N / gridDim.x;
+    for (int64_t r = ra; r < rb; ++r) {
+      const uint32_t m = k.uflags[kMarkB * r + 2] & 7u;
+      for (int part = 0; part < 3; ++part)
+        if ((m >> part) & 1u) {
+          if (x >= s0 && x < s1) slist[x - s0] = (int)(r << 3) | part;
+          ++x;
+        }
+    }
+    u1 = __builtin_amdgcn_readfirstlane((int)(s1 - s0));   // (the barrier after the setup publishes slist)
+  } else {
+    const int64_t units = 3 * k.B;
+    const int64_t per = (units + gridDim.x - 1) / gridDim.x;
+    u0 = (int64_t)blockIdx.x * per;
+    u1 = u0 + per < units ? u0 + per : units;
+  }
   const int pp = lane & 15;
   // the staging pool: 80 KiB
   uint32_t* const st_raw = sc_dyn + 2 * ((k.nbins + 3) & ~3);   // 16-B aligned after the counters
@@ -1809,8 +1849,9 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     q.g0 = q.g1 = 0.f;
     q.tb = q.tw = nullptr;
     if (q.act) {
-      const int64_t ray = unit_ray(u / 3);
-      const int i = 64 * (int)(u % 3) + lane;       // fine sample
+      const int code = use_list ? __builtin_amdgcn_readfirstlane(slist[u]) : 0;
+      const int64_t ray = use_list ? (int64_t)(code >> 3) : unit_ray(u / 3);
+      const int i = 64 * (use_list ? (code & 3) : (int)(u % 3)) + lane;   // fine sample
       load_ray(k.rays, ray, q.r);
       ray_point(q.r, k.z_fine[ray * kSf + i], q.pt);
 #pragma unroll
@@ -2351,61 +2392,82 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
     return;
   }
   const int64_t w = (int64_t)(blockIdx.x - (k.lout ? 1 : 0)) * kFwdWaves + wave;
-  if (w >= 2 * k.B) return;
+  // the two waves of a ray (coarse 2r, fine 2r + 1) share the workgroup: the
+  // coarse wave's nonzero-sample mask reaches the fine wave through LDS
+  __shared__ unsigned long long cmask[kFwdWaves / 2];
+  const bool active = w < 2 * k.B;
   const int64_t ray = w >> 1;
   const bool fine = (w & 1) != 0;
-  const int S = fine ? kSf : kSc;
-  float* zb = lds[wave];
-  float* rawb = zb + kSf;
-  const float* zsrc = (fine ? k.z_fine : k.z_coarse) + ray * S;
-  const float* rsrc = (fine ? k.raw_f : k.raw_c) + ray * S * 4;
-  for (int j = lane; j < S; j += 64) {
-    zb[j] = zsrc[j];
-    *reinterpret_cast<float4*>(rawb + 4 * j) = *reinterpret_cast<const float4*>(rsrc + 4 * j);
-  }
-  lds_fence_wave();
-  Ray r;
-  load_ray(k.rays, ray, r);
-  CompGrad g;
-  const float* grgb = fine ? k.g_rgb : k.g_rgb0;
-  const float* gacc = fine ? k.g_acc : k.g_acc0;
-  const float* gdep = fine ? k.g_depth : k.g_depth0;
-  const float* gent = fine ? k.g_sparsity : k.g_sparsity0;
-  if (k.lout) {   // the training loss's gradients (hn_loss_bwd_elem's op forms, g_loss = 1)
-    const float* x = fine ? k.lrgb : k.lrgb0;
-    g.has_rgb = g.has_entropy = true;
-    g.has_acc = g.has_depth = false;
+  float* rawb = lds[wave] + kSf;
+  if (active) {
+    const int S = fine ? kSf : kSc;
+    float* zb = lds[wave];
+    const float* zsrc = (fine ? k.z_fine : k.z_coarse) + ray * S;
+    const float* rsrc = (fine ? k.raw_f : k.raw_c) + ray * S * 4;
+    for (int j = lane; j < S; j += 64) {
+      zb[j] = zsrc[j];
+      *reinterpret_cast<float4*>(rawb + 4 * j) = *reinterpret_cast<const float4*>(rsrc + 4 * j);
+    }
+    lds_fence_wave();
+    Ray r;
+    load_ray(k.rays, ray, r);
+    CompGrad g;
+    const float* grgb = fine ? k.g_rgb : k.g_rgb0;
+    const float* gacc = fine ? k.g_acc : k.g_acc0;
+    const float* gdep = fine ? k.g_depth : k.g_depth0;
+    const float* gent = fine ? k.g_sparsity : k.g_sparsity0;
+    if (k.lout) {   // the training loss's gradients (hn_loss_bwd_elem's op forms, g_loss = 1)
+      const float* x = fine ? k.lrgb : k.lrgb0;
+      g.has_rgb = g.has_entropy = true;
+      g.has_acc = g.has_depth = false;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) g.rgb[c] = k.lgm * (2.f * (x[3 * ray + c] - k.ltarget[3 * ray + c]));
-    g.acc = g.depth = 0.f;
-    g.entropy = k.lsparse;
-  } else {
-    g.has_rgb = grgb != nullptr;
-    g.has_acc = gacc != nullptr;
-    g.has_depth = gdep != nullptr;
-    g.has_entropy = gent != nullptr;
+      for (int c = 0; c < 3; ++c) g.rgb[c] = k.lgm * (2.f * (x[3 * ray + c] - k.ltarget[3 * ray + c]));
+      g.acc = g.depth = 0.f;
+      g.entropy = k.lsparse;
+    } else {
+      g.has_rgb = grgb != nullptr;
+      g.has_acc = gacc != nullptr;
+      g.has_depth = gdep != nullptr;
+      g.has_entropy = gent != nullptr;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) g.rgb[c] = g.has_rgb ? grgb[3 * ray + c] : 0.f;
-    g.acc = g.has_acc ? gacc[ray] : 0.f;
-    g.depth = g.has_depth ? gdep[ray] : 0.f;
-    g.entropy = g.has_entropy ? gent[ray] : 0.f;
+      for (int c = 0; c < 3; ++c) g.rgb[c] = g.has_rgb ? grgb[3 * ray + c] : 0.f;
+      g.acc = g.has_acc ? gacc[ray] : 0.f;
+      g.depth = g.has_depth ? gdep[ray] : 0.f;
+      g.entropy = g.has_entropy ? gent[ray] : 0.f;
+    }
+    const float* noise = fine ? (k.noise_f ? k.noise_f + ray * S : nullptr)
+                              : (k.noise_c ? k.noise_c + ray * S : nullptr);
+    const float* graw = (fine && k.g_raw_f) ? k.g_raw_f + ray * S * 4 : nullptr;
+    float* dst = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0)) * 4;
+    if (fine)
+      composite_bwd<kSf / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
+    else
+      composite_bwd<kSc / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
+    lds_fence_wave();
+    uint32_t nzu = 0u;   // bit u: a sample of MLP unit u (64 samples) has a nonzero d raw
+    for (int j = lane; j < S; j += 64) {
+      const float4 d = *reinterpret_cast<const float4*>(rawb + 4 * j);
+      *reinterpret_cast<float4*>(dst + 4 * j) = d;
+      nzu |= (__ballot(draw_nonzero(d)) != 0ull ? 1u : 0u) << (j >> 6);
+    }
+    if (lane == 0) k.uflags[kMarkB * ray + (fine ? 1 : 0)] = (uint8_t)nzu;
+    if (!fine) cmask[wave >> 1] = __ballot(draw_nonzero(*reinterpret_cast<const float4*>(rawb + 4 * lane)));
   }
-  const float* noise = fine ? (k.noise_f ? k.noise_f + ray * S : nullptr)
-                            : (k.noise_c ? k.noise_c + ray * S : nullptr);
-  const float* graw = (fine && k.g_raw_f) ? k.g_raw_f + ray * S * 4 : nullptr;
-  float* dst = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0)) * 4;
-  if (fine)
-    composite_bwd<kSf / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
-  else
-    composite_bwd<kSc / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
-  lds_fence_wave();
-  uint32_t nzu = 0u;   // bit u: a sample of MLP unit u (64 samples) has a nonzero d raw
-  for (int j = lane; j < S; j += 64) {
-    const float4 d = *reinterpret_cast<const float4*>(rawb + 4 * j);
-    *reinterpret_cast<float4*>(dst + 4 * j) = d;
-    nzu |= (__ballot(draw_nonzero(d)) != 0ull ? 1u : 0u) << (j >> 6);
+  __syncthreads();
+  if (active && fine) {
+    // the scatter's marks: bit u = a sample of fine unit u, or its coarse twin
+    // (the same point, fine_src < 64), has a nonzero d raw -- the unit has
+    // feature grads to scatter (scatter_bins_kernel's unit lists)
+    const unsigned long long cm = cmask[wave >> 1];
+    uint32_t su = 0u;
+    for (int j = lane; j < kSf; j += 64) {
+      const int src = k.fine_src[ray * kSf + j];
+      const bool nz = draw_nonzero(*reinterpret_cast<const float4*>(rawb + 4 * j)) ||
+                      (src < kSc && ((cm >> src) & 1ull) != 0ull);
+      su |= (__ballot(nz) != 0ull ? 1u : 0u) << (j >> 6);
+    }
+    if (lane == 0) k.uflags[kMarkB * ray + 2] = (uint8_t)su;
   }
-  if (lane == 0) k.uflags[2 * ray + (fine ? 1 : 0)] = (uint8_t)nzu;
 }
 
 // acc[base + n*ld + k] += D[n - n0][k - k0] for n < nmax, k < kmax (LDS),
@@ -2540,8 +2602,8 @@ void render_bwd_kernel(B1K k) {
     int* scn = reinterpret_cast<int*>(slots);                // [2][kB1Waves] wave totals
     const int nthr = 64 * kB1Waves, t = threadIdx.x;
     const int64_t R = (k.B + nthr - 1) / nthr, ra = (int64_t)t * R, rb = ra + R < k.B ? ra + R : k.B;
-    auto cmark = [&](int64_t r) -> int { return k.skip_zero ? (int)(k.uflags[2 * r] & 1u) : 1; };
-    auto fmark = [&](int64_t r) -> uint32_t { return k.skip_zero ? (uint32_t)(k.uflags[2 * r + 1] & 7u) : 7u; };
+    auto cmark = [&](int64_t r) -> int { return k.skip_zero ? (int)(k.uflags[kMarkB * r] & 1u) : 1; };
+    auto fmark = [&](int64_t r) -> uint32_t { return k.skip_zero ? (uint32_t)(k.uflags[kMarkB * r + 1] & 7u) : 7u; };
     int sc = 0, sf = 0;
     for (int64_t r = ra; r < rb; ++r) {
       sc += cmark(r);
@@ -3059,7 +3121,7 @@ static int bwd_mode(const hn_render_cfg* c, int64_t n_rays) {
   return kModeSplit;
 }
 // Workspace (floats): packed coarse + fine weights | dW slabs [256][2][9344] |
-// coarse-pass feature grads [n][64][32] | d raw [n][256][4] | unit marks [n][2] u8 (padded) | split: fine
+// coarse-pass feature grads [n][64][32] | d raw [n][256][4] | unit marks [n][4] u8 + wave split | split: fine
 // feature grads [n][6][1024] and the records (bin_geom).
 struct WsLayout {
   size_t dfeat_f, bins, total;
@@ -3068,7 +3130,7 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4 +
-              ((n + 3) & ~(size_t)3);   // + the unit marks, 2 bytes per ray (B1K::uflags)
+              ((n * kMarkB / 4 + 1 + 3) & ~(size_t)3);   // + the unit marks (B1K::uflags) and the wave split
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -3311,8 +3373,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.dfeat = dfeat;
   k.draw = draw;
   k.uflags = uflags;
-  // the split schedule's coarse / fine wave split, after the marks (2 bytes per ray)
-  k.gsplit = reinterpret_cast<int32_t*>(uflags + ((2 * (size_t)a->n_rays + 3) & ~(size_t)3));
+  // the split schedule's coarse / fine wave split, after the marks
+  k.gsplit = reinterpret_cast<int32_t*>(uflags + kMarkB * (size_t)a->n_rays);
   k.ltarget = k.lrgb = k.lrgb0 = k.lsp = k.lsp0 = k.ltv = nullptr;
   k.n_tv = 0;
   k.lgm = k.lsparse = k.lworld = k.lsparse_w = k.ltv_w = 0.f;
@@ -3417,6 +3479,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.scramble = k.scramble;
     sk.skip_zero = k.skip_zero;
     sk.gsplit = k.gsplit;
+    sk.uflags = k.uflags;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
     sk.dfeat_f = k.dfeat_f;
