@@ -60,7 +60,7 @@ class HnRenderFwdArgs(C.Structure):
                 ("rgb", _P), ("depth", _P), ("acc", _P), ("sparsity", _P),
                 ("rgb0", _P), ("depth0", _P), ("acc0", _P), ("sparsity0", _P),
                 ("z_std", _P), ("z_coarse", _P), ("z_fine", _P), ("raw_c", _P), ("raw_f", _P),
-                ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32)]
+                ("fine_src", _P), ("feat", _P), ("weights_packed", C.c_int32), ("skip_dead_color", C.c_int32)]
 
 
 class HnRadamTensor(C.Structure):

@@ -218,7 +218,7 @@ HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 
 // the fused forward computes it once per ray and seeds every tile with it).
 template <bool MASKS = false, typename C0Init, typename Src>
 HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, MlpAct& a, f32x16& c2,
-                             int lane);
+                             int lane, bool skip_dead = false);
 template <bool MASKS = false, typename C0Init>
 HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0Init&& c0init,
                             MlpAct& a, f32x16& c2, int lane) {
@@ -226,7 +226,7 @@ HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0I
 }
 template <bool MASKS, typename C0Init, typename Src>
 HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, MlpAct& a, f32x16& c2,
-                             int lane) {
+                             int lane, bool skip_dead) {
   a.m[0] = a.m[1] = a.m[2] = 0u;
   // sigma_net.0: 32 -> 64, ReLU
   // (Both output blocks of a GEMM sharing one B split per chunk, as the
@@ -241,6 +241,20 @@ HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, 
   if constexpr (MASKS) asm volatile("" : "+v"(a.m[0]));
   // sigma_net.1: 64 -> 16 (sigma, geo15), no activation
   a.s1 = gemm_src<R_F1>(P, 0, zero16(), lane, [&](int s) { return a.h0[s >> 4][s & 15]; });
+  // skip_dead (the trainer's forward, no raw noise): a tile whose 32 raw
+  // sigmas (row 0, lanes 0-31) are all <= 0 has alpha = 0 and weight 0 at
+  // every sample (raw2outputs, run_nerf_helpers.py:577-628), so its colours
+  // enter no output and no gradient: the colour net is not evaluated (raw rgb
+  // written as 0, its ReLU masks 0) and the weight stream restarts at the next
+  // tile's first chunk
+  if (skip_dead && __ballot(lane < 32 && a.s1[0] > 0.f) == 0ull) {
+    c2 = zero16();
+    if constexpr (Src::kRing) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slot's pending fill has landed
+      ring_fill(P.P, P.slot, fwd_chunk_off(kFwdSeq[0]), lane);
+    }
+    return;
+  }
   // color_net.0: [sh16 | geo15] -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {

@@ -63,6 +63,7 @@ struct RenderK {
   uint8_t* fine_src;
   float* feat;    // [B][8 tiles][1024] saved features or NULL
   int feat_nt;    // saved features stored nontemporally (tables past the MALL)
+  int skip_dead;  // hn_render_fwd_args.skip_dead_color
 };
 
 
@@ -348,7 +349,7 @@ void render_fwd_kernel(RenderK k) {
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
-                           a, c2, lane);
+                           a, c2, lane, k.skip_dead && k.noise_c == nullptr);
     if (k.feat) store_masks(k.feat, ray, tau, lane, a.m, k.feat_nt != 0);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
@@ -428,7 +429,7 @@ void render_fwd_kernel(RenderK k) {
     MlpAct a;
     f32x16 c2;
     mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
-                           a, c2, lane);
+                           a, c2, lane, k.skip_dead && k.noise_f == nullptr);
     if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m, k.feat_nt != 0);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
@@ -3198,6 +3199,7 @@ extern "C" int32_t hn_render_fwd(const hn_render_cfg* cfg, const hn_render_fwd_a
   // -8 us); past it they are streamed (config 3, T=22, cached: forward
   // 633 -> 682 us)
   k.feat_nt = cfg->grid.log2_hashmap_size > 20;
+  k.skip_dead = a->skip_dead_color != 0;
   const unsigned blocks = (unsigned)((a->n_rays + kFwdBlockWaves - 1) / kFwdBlockWaves);
   hipLaunchKernelGGL(render_fwd_kernel, dim3(blocks), dim3(64 * kFwdBlockWaves), 0, s, k);
 #if HN_PROFILE

@@ -222,12 +222,15 @@ class RenderState:
 
 
 def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None,
-               weights_packed=False):
+               weights_packed=False, skip_dead_color=False):
     """hn_render_fwd (run_nerf_helpers.py:464-574, forward).  Returns the
     output dict and a RenderState (None when keep_feat is False).  wsb: the
     caller's workspace (uint8, >= workspace_bytes; default a fresh one);
     weights_packed: it already holds ws's packed copies (render_bwd with
-    repack=True since the last change of ws)."""
+    repack=True since the last change of ws).  skip_dead_color (ABI 14, the
+    trainer): tiles whose 32 raw sigmas are all <= 0 skip the colour net --
+    rgb, depth, acc, the entropies and every gradient unchanged, the raw rgb
+    of those samples written as 0."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -262,6 +265,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     else:
         nbytes = wsb.numel() * wsb.element_size()
     a.weights_packed = 1 if weights_packed else 0
+    a.skip_dead_color = 1 if skip_dead_color else 0
     t0 = TIMER.begin("render_fwd")
     L.check(L.lib().hn_render_fwd(cfg, a, L.ptr(wsb), nbytes, L.stream(dev)), "render_fwd")
     TIMER.end("render_fwd", t0)

@@ -850,8 +850,11 @@ class Trainer:
         nb = HF.L.lib().hn_render_workspace_bytes(self._cfg, rays.shape[0])
         if self._rws is None or self._rws.numel() < nb:
             self._rws, self._pk = torch.empty(nb, dtype=torch.uint8, device=self.device), None
+        # the colour net of tiles without any density is skipped (the trainer never
+        # returns raw rgb; with dense_bwd everything is computed, for the A/B)
         out, st = HF.render_fwd(self._cfg, rays, self._t_vals, t_rand, u, None, None, table, self._ws, True,
-                                wsb=self._rws, weights_packed=self._pk is not None and self._pk == self._pack_key())
+                                wsb=self._rws, weights_packed=self._pk is not None and self._pk == self._pack_key(),
+                                skip_dead_color=not self.dense_bwd)
         self._pk = None
         if pf:
             self._prefetch(i + 1)

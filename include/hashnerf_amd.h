@@ -206,6 +206,12 @@ typedef struct hn_render_fwd_args {
   int32_t weights_packed;   /* ABI 13: nonzero = `workspace` already holds both nets' packed MFMA
                                copies of these weights (an hn_render_bwd with repack wrote them and the
                                weights are unchanged since): no packing launch */
+  int32_t skip_dead_color;  /* ABI 14: nonzero (and no noise for that pass) = a tile of 32 samples
+                               whose raw sigmas are all <= 0 -- alpha 0 and weight 0 at every sample,
+                               so its colours enter no output and no gradient -- skips the colour
+                               net: raw_c / raw_f rgb of those samples are written as 0 (rgb, depth,
+                               acc, the entropies and every gradient unchanged).  0 = every sample's
+                               raw rgb computed (the reference's `raw` output) */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {
