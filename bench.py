@@ -473,6 +473,23 @@ def main():
         host.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
     host_ms = 1e3 * sorted(host)[len(host) // 2]
+    # what the exact-zero skips had to work with, from one more step's raw
+    # sigmas (a sample with raw sigma <= 0 has alpha = 0: no gradient, and its
+    # colour enters no output).  Lower bounds of the skipped shares: the
+    # kernels' own marks also count samples whose d raw vanishes otherwise
+    HF.DEBUG_KEEP = True
+    tr.step()
+    HF.DEBUG_KEEP = False
+    dc, df = HF.LAST["raw_c"][..., 3] <= 0, HF.LAST["raw_f"][..., 3] <= 0
+    sparsity = {
+        "coarse_units_without_density": round(dc.all(-1).float().mean().item(), 4),
+        "fine_units_without_density": round(df.view(-1, 3, 64).all(-1).float().mean().item(), 4),
+        "tiles_without_density": round(torch.cat([dc.view(-1, 32), df.view(-1, 32)]).all(-1).float().mean().item(), 4),
+        "samples_without_density": round(torch.cat([dc.reshape(-1), df.reshape(-1)]).float().mean().item(), 4),
+        "skips": "" if args.dense_bwd else
+        "MLP-backward units and scatter units without gradient, zero records, and the forward's colour net "
+        "on tiles without density (hn_render_cfg.dense_bwd = 0, skip_dead_color): every output and "
+        "gradient as computed densely (tests/test_gpu_driver.py::test_zero_gradient_skip_bitwise)"}
     B = cfg["N_rand"]
     value = world * B * args.steps / dt
     if rank == 0:
@@ -559,6 +576,7 @@ def main():
             line["roofline"].update(atomic_requests=round(atomics), atomic_Greq_per_s=round(rate, 2),
                                     atomic_peak_Greq_per_s=ATOMIC_PEAK_GREQ,
                                     atomic_frac=round(rate / ATOMIC_PEAK_GREQ, 3))
+        line["sparsity"] = sparsity
         if xchg is not None:
             line["exchange"] = xchg
         if world == 1 and not args.no_cpu_baseline:

@@ -290,6 +290,9 @@ void render_fwd_kernel(RenderK k) {
   // XCD-aware: workgroup b runs on XCD b % 8, so consecutive ray groups of a
   // spatially ordered batch go to one XCD and share its L2
   const int64_t nb = gridDim.x;
+  // (round 6, r06k: chunks of 4 or 16 ray groups dealt round-robin over the
+  // XCDs, or no XCD mapping at all, were no faster: 234.9 / 228.8 / 240.4 us
+  // against 229.4 us -- the forward's per-XCD work is balanced already)
   const int64_t grp = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
   const int64_t ray = grp * kFwdBlockWaves + wave;
   if (ray >= k.B) return;
