@@ -98,9 +98,12 @@ struct B1K {
   float lgm, lsparse, lworld, lsparse_w, ltv_w;
   float* lout;
   int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
-  uint8_t* uflags;      // [B][kMarkB] unit marks (composite pre-pass): [0] coarse, [1] fine MLP units with a
-                        // nonzero d raw, [2] fine units with a nonzero sample or coarse twin (the scatter's)
-  int32_t* gsplit;      // split schedule: the waves g < *gsplit ran coarse units (slab_reduce_block)
+  uint8_t* uflags;      // [B][kMarkB] marks (composite pre-pass): [0] coarse, [1] fine MLP tiles with a
+                        // nonzero d raw, [2] fine units (64 samples) with a nonzero sample or coarse twin
+                        // (the scatter's)
+  int32_t* lmeta;       // work lists (render_lists_kernel): [0] coarse tiles, [1] fine tiles, [2] scatter
+                        // units, [3] gsplit: the MLP waves g < gsplit run coarse tiles (slab_reduce_block)
+  int32_t* lists;       // coarse tile codes [2B] | fine tile codes [6B] | scatter unit codes [3B]
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -1625,8 +1628,8 @@ struct ScK {
   const float* draw;      // [B][64 + 192][4] d raw (composite pre-pass): zero = no feature grads to read
   int32_t scramble;       // the MLP backward's ray permutation (B1K::scramble; 0: identity)
   int32_t skip_zero;      // exact-zero skipping (!hn_render_cfg.dense_bwd)
-  const int32_t* gsplit;  // the MLP backward's coarse / fine wave split (slab_reduce_block)
-  const uint8_t* uflags;  // [B][kMarkB] unit marks (byte 2: fine units with feature grads), or null
+  const int32_t* lmeta;   // render_lists_kernel's counts ([2] scatter units, [3] the MLP waves' split)
+  const int32_t* slist;   // its scatter unit codes (ray << 3 | part), or null: every unit
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
@@ -1735,40 +1738,21 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   bw.cap = (uint32_t)k.bin_cap;
   bw.shift = (uint32_t)k.bin_shift;
   // The block's units.  With exact-zero skipping: its slice of the list of
-  // fine units that have feature grads to scatter (the composite pre-pass's
-  // marks, byte 2), the list in ray order and cut into equal slices over the
-  // blocks -- every block the same share of the work, whatever the scene
-  // leaves nonzero; every block computes the same prefix over the marks.
-  // Otherwise (dense_bwd, or more than kScListCap units per block) every unit,
-  // the rays permuted as the MLP backward's (unit_ray).
-  constexpr int kScListCap = 256;
-  __shared__ int slist[kScListCap];
-  __shared__ int sc_tot[kScWaves];
-  const bool use_list = k.skip_zero && k.uflags != nullptr && 3 * k.B <= (int64_t)kScListCap * gridDim.x;
+  // fine units that have feature grads to scatter (render_lists_kernel, from
+  // the composite pre-pass's marks), the list in ray order and cut into equal
+  // slices over the blocks -- every block the same share of the work,
+  // whatever the scene leaves nonzero; each wave holds its units' codes in a
+  // register (lane j: round j).  Otherwise (dense_bwd) every unit, the rays
+  // permuted as the MLP backward's (unit_ray).
+  const bool use_list = k.slist != nullptr;
   int64_t u0 = 0, u1 = 0;
+  int ucode = 0;   // lane j: the code of this wave's unit of round j
   if (use_list) {
-    const int64_t R = (k.B + blockDim.x - 1) / blockDim.x, ra = (int64_t)threadIdx.x * R;
-    const int64_t rb = ra + R < k.B ? ra + R : k.B;
-    int cnt = 0;
-    for (int64_t r = ra; r < rb; ++r) cnt += __builtin_popcount(k.uflags[kMarkB * r + 2] & 7u);
-    const int inc = (int)wave_incl_sum((double)cnt);
-    if (lane == 63) sc_tot[wave] = inc;
-    __syncthreads();
-    int64_t x = inc - cnt, N = 0;
-    for (int q = 0; q < kScWaves; ++q) {
-      if (q < wave) x += sc_tot[q];
-      N += sc_tot[q];
-    }
-    const int64_t s0 = (int64_t)blockIdx.x * N / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * N / gridDim.x;
-    for (int64_t r = ra; r < rb; ++r) {
-      const uint32_t m = k.uflags[kMarkB * r + 2] & 7u;
-      for (int part = 0; part < 3; ++part)
-        if ((m >> part) & 1u) {
-          if (x >= s0 && x < s1) slist[x - s0] = (int)(r << 3) | part;
-          ++x;
-        }
-    }
-    u1 = __builtin_amdgcn_readfirstlane((int)(s1 - s0));   // (the barrier after the setup publishes slist)
+    const int64_t Ns = __builtin_amdgcn_readfirstlane(k.lmeta[2]);
+    const int64_t s0 = (int64_t)blockIdx.x * Ns / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * Ns / gridDim.x;
+    u1 = s1 - s0;
+    const int64_t uj = wave + (int64_t)lane * kScWaves;
+    if (lane < 64 && uj < u1) ucode = k.slist[s0 + uj];
   } else {
     const int64_t units = 3 * k.B;
     const int64_t per = (units + gridDim.x - 1) / gridDim.x;
@@ -1853,7 +1837,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     q.g0 = q.g1 = 0.f;
     q.tb = q.tw = nullptr;
     if (q.act) {
-      const int code = use_list ? __builtin_amdgcn_readfirstlane(slist[u]) : 0;
+      const int code = use_list ? __builtin_amdgcn_readlane(ucode, (int)it) : 0;
       const int64_t ray = use_list ? (int64_t)(code >> 3) : unit_ray(u / 3);
       const int i = 64 * (use_list ? (code & 3) : (int)(u % 3)) + lane;   // fine sample
       load_ray(k.rays, ray, q.r);
@@ -2065,7 +2049,7 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       const int vb = vb_sh;
       if (vb >= kSlabVBlocks) break;
       slab_reduce_block(k.slab, kBwdBlocks, k.dc, k.df, k.overwrite_mlp, vb, part, k.has_mstep ? k.mstep : nullptr,
-                        k.gsplit);
+                        k.lmeta + 3);
     }
   }
 }
@@ -2295,28 +2279,33 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 // unit templates): 87 KB of code -> ~25 KB, under the 64 KB instruction cache
 // two CUs share (wave 0 ran the coarse copies, waves 1-3 the fine ones, at
 // the same time).
-// A unit (two tiles) whose 64 samples all have d raw = 0 (raw2outputs'
-// backward gives exactly that to every sample with relu(sigma) = 0: alpha =
-// 0, weight 0, run_nerf_helpers.py:577-628) has an exactly zero MLP
-// backward: zero feature grads, and it adds 0 to every dW accumulator.  Such
-// units are skipped -- the same results bitwise (an accumulator plus exact
-// zeros is unchanged) for ~2/3 of the units of a trained scene (config 2:
-// 57 % of the coarse and 70 % of the fine tiles, scripts/zero_grad_frac.py).
+// A tile whose 32 samples all have d raw = 0 (raw2outputs' backward gives
+// exactly that to every sample with relu(sigma) = 0: alpha = 0, weight 0,
+// run_nerf_helpers.py:577-628) has an exactly zero MLP backward: zero
+// feature grads, and it adds 0 to every dW accumulator.  Such tiles are
+// skipped -- the same results (an accumulator plus exact zeros is unchanged)
+// for ~2/3 of the tiles of a trained scene (config 2: 57 % of the coarse and
+// 70 % of the fine tiles, scripts/zero_grad_frac.py).
 // Nothing is stored for them: the scatter kernel reads a sample's feature
 // grads only where its own d raw (or its coarse twin's) is nonzero.  The
 // weight ring is aligned to the tile period, so a skipped unit leaves it
-// ready for the next one.  The composite pre-pass marks the units with a
-// nonzero d raw (B1K::uflags), and each wave iterates over the set bits of a
-// ballot of its units' marks: the same loop shape as over every unit (a
-// per-unit test inside the loop made the register allocator spill).
-HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float* X, DW& dw, WRing& wr) {
+// ready for the next one.  The composite pre-pass marks the tiles with a
+// nonzero d raw (B1K::uflags), and the waves run lists of the marked tiles
+// (render_bwd_kernel): the same loop shape as over every tile (a per-tile
+// test inside the loop made the register allocator spill).
+// new_ray: the previous tile of this wave was another ray's (or none), so
+// the ray's SH operand image and color_net.0's SH rows (c0sh) are set up;
+// otherwise they are still in the wave's LDS from that tile.
+HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int tile, bool fine, float* X, DW& dw, WRing& wr,
+                          bool new_ray = true) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
-  const int tile0 = 2 * part;
-  const float* drs = k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile0 + p) * 4;
-  float4 dr[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) dr[t] = *reinterpret_cast<const float4*>(drs + 128 * t);
+  const float4 dr = *reinterpret_cast<const float4*>(
+      k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile + p) * 4);
+  const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
+  C0Sh c0sh;
+  c0sh.lds = X + kC0shF;
+  if (new_ray) {
   Ray r;
   load_ray(k.rays, ray, r);
   float sh8[8], shx8[8];
@@ -2330,8 +2319,6 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
       put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h + 1, w[2], w[3]);
     }
   }
-  const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
-  C0Sh c0sh;
   {
     float* cl = X + kC0shF;
 #pragma unroll
@@ -2344,28 +2331,21 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int part, bool fine, float*
               f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
     }
     lds_fence_wave();
-    c0sh.lds = cl;
   }
-  const int ctile = (fine ? kSc / 32 : 0) + tile0;
-  f32x16 feat, featn;
+  }
+  const int ctile = (fine ? kSc / 32 : 0) + tile;
+  f32x16 feat;
   load_feat(k.feat, ray, ctile, lane, feat);
-  load_feat(k.feat, ray, ctile + 1, lane, featn);
-  // this unit's feature-grad tiles (the saved-feature tile order of both passes)
-  f32x4* dst0 = fine ? reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + tile0) * 1024)
-                     : reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)tile0 * 1024);
-#pragma clang loop unroll(disable)
-  for (int t = 0; t < 2; ++t) {
-    const float4 drt = t ? dr[1] : dr[0];
-    uint32_t sm[3] = {0u, 0u, 0u};
-    load_masks(k.feat, ray, ctile + t, lane, sm);
-    const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, drt, dw, sm);
-    f32x4* dst = dst0 + 256 * t;
+  uint32_t sm[3] = {0u, 0u, 0u};
+  load_masks(k.feat, ray, ctile, lane, sm);
+  const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, dr, dw, sm);
+  // this tile's feature grads (the saved-feature tile order of both passes)
+  f32x4* dst = fine ? reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + tile) * 1024)
+                    : reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)tile * 1024);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const f32x4 v = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
-      __builtin_nontemporal_store(v, dst + 64 * c + lane);   // read once, by the scatter
-    }
-    feat = featn;
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 v = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
+    __builtin_nontemporal_store(v, dst + 64 * c + lane);   // read once, by the scatter
   }
 }
 
@@ -2448,11 +2428,13 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
     else
       composite_bwd<kSc / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
     lds_fence_wave();
-    uint32_t nzu = 0u;   // bit u: a sample of MLP unit u (64 samples) has a nonzero d raw
+    uint32_t nzu = 0u;   // bit t: a sample of MLP tile t (32 samples) has a nonzero d raw
     for (int j = lane; j < S; j += 64) {
       const float4 d = *reinterpret_cast<const float4*>(rawb + 4 * j);
       *reinterpret_cast<float4*>(dst + 4 * j) = d;
-      nzu |= (__ballot(draw_nonzero(d)) != 0ull ? 1u : 0u) << (j >> 6);
+      const uint64_t b = __ballot(draw_nonzero(d));
+      nzu |= ((uint32_t)b != 0u ? 1u : 0u) << (2 * (j >> 6));
+      nzu |= ((uint32_t)(b >> 32) != 0u ? 1u : 0u) << (2 * (j >> 6) + 1);
     }
     if (lane == 0) k.uflags[kMarkB * ray + (fine ? 1 : 0)] = (uint8_t)nzu;
     if (!fine) cmask[wave >> 1] = __ballot(draw_nonzero(*reinterpret_cast<const float4*>(rawb + 4 * lane)));
@@ -2536,6 +2518,75 @@ HN_DEV void dw_zero(DW& dw) {
   for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
 }
 
+// The backward's work lists (round 6), from the composite pre-pass's marks
+// (B1K::uflags; every tile and unit with dense_bwd): the coarse tiles, the
+// fine tiles and the scatter's fine units with feature grads, each in ray
+// order, as codes (ray << 3 | tile or part); their lengths and the MLP
+// waves' coarse / fine split.  One 1024-thread workgroup: each thread a run
+// of rays, a block-wide prefix of its counts, then its codes.  (Computed
+// redundantly by every block of the two kernels that use them it cost the
+// MLP backward ~28 us.)
+constexpr int kListThreads = 1024;
+__global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
+  __shared__ int tot[3][kListThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t R = (k.B + kListThreads - 1) / kListThreads, ra = (int64_t)t * R;
+  const int64_t rb = ra + R < k.B ? ra + R : k.B;
+  // bytes [coarse tiles (2 bits), fine tiles (6), scatter units (3), -]
+  auto mword = [&](int64_t r) -> uint32_t {
+    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0x073f03u;
+  };
+  int nc = 0, nf = 0, ns = 0;
+  for (int64_t r = ra; r < rb; ++r) {
+    const uint32_t w = mword(r);
+    nc += __builtin_popcount(w & 3u);
+    nf += __builtin_popcount((w >> 8) & 63u);
+    ns += __builtin_popcount((w >> 16) & 7u);
+  }
+  const int ic = (int)wave_incl_sum((double)nc), jf = (int)wave_incl_sum((double)nf), ks = (int)wave_incl_sum((double)ns);
+  if (lane == 63) {
+    tot[0][wave] = ic;
+    tot[1][wave] = jf;
+    tot[2][wave] = ks;
+  }
+  __syncthreads();
+  int64_t xc = ic - nc, xf = jf - nf, xs = ks - ns, Nc = 0, Nf = 0, Ns = 0;
+  for (int q = 0; q < kListThreads / 64; ++q) {
+    if (q < wave) {
+      xc += tot[0][q];
+      xf += tot[1][q];
+      xs += tot[2][q];
+    }
+    Nc += tot[0][q];
+    Nf += tot[1][q];
+    Ns += tot[2][q];
+  }
+  int32_t* lc = k.lists;
+  int32_t* lf = lc + 2 * k.B;
+  int32_t* ls = lf + 6 * k.B;
+  for (int64_t r = ra; r < rb; ++r) {
+    const uint32_t w = mword(r);
+    for (int i = 0; i < 2; ++i)
+      if ((w >> i) & 1u) lc[xc++] = (int32_t)(r << 3) | i;
+    for (int i = 0; i < 6; ++i)
+      if ((w >> (8 + i)) & 1u) lf[xf++] = (int32_t)(r << 3) | i;
+    for (int i = 0; i < 3; ++i)
+      if ((w >> (16 + i)) & 1u) ls[xs++] = (int32_t)(r << 3) | i;
+  }
+  if (t == 0) {
+    const int G = kB1Waves * kBwdBlocks;
+    int gc = Nc > 0 ? G : 0;   // MLP waves on the coarse list, in proportion to the lists
+    if (Nc > 0 && Nf > 0) {
+      gc = (int)((2 * (int64_t)G * Nc + Nc + Nf) / (2 * (Nc + Nf)));
+      gc = gc < 1 ? 1 : (gc > G - 1 ? G - 1 : gc);
+    }
+    k.lmeta[0] = (int32_t)Nc;
+    k.lmeta[1] = (int32_t)Nf;
+    k.lmeta[2] = (int32_t)Ns;
+    k.lmeta[3] = gc;
+  }
+}
+
 // One persistent block per CU owns rays blockIdx.x + i * gridDim.x.  Wave 0
 // first runs the block's coarse units (MLP backward of network_fn only) and
 // publishes each ray's coarse feature grads through an LDS counter; then it
@@ -2589,102 +2640,41 @@ void render_bwd_kernel(B1K k) {
   if (wave == kMW && !SPLIT) {
     ring_drain<CAP>(k, ring, V, 2 * kSf / 64 * n_rays);
   } else if (SPLIT) {
-    // Balanced unit lists (round 6).  The units with a nonzero d raw (the
+    // Balanced tile lists (round 6).  The tiles with a nonzero d raw (the
     // composite pre-pass's marks; all of them with dense_bwd) form two lists in
-    // ray order -- coarse units, then fine units (ray, part) -- and the
-    // kB1Waves x nb MLP waves g = wave * nb + block split them: the first
-    // gsplit waves the coarse list, the others the fine list, in contiguous
-    // slices of equal length (gsplit in proportion to the two lists).  Every
-    // wave then runs ~1/1024 of the work, whatever the scene leaves nonzero;
-    // each wave keeps one net's dW and stores it to slab g, which the scatter
-    // kernel's slab reduction sums in g order: deterministic (the split is a
-    // function of the marks alone).  Every block computes the same prefix sums
-    // over the marks and materializes its 4 waves' slices in LDS (V), in
-    // rounds of kUlCap units (one round unless a wave has more).
-    constexpr int kUlCap = kVoxF / kB1Waves;                 // unit codes per wave and round
-    int* ul = reinterpret_cast<int*>(V);
-    int* scn = reinterpret_cast<int*>(slots);                // [2][kB1Waves] wave totals
-    const int nthr = 64 * kB1Waves, t = threadIdx.x;
-    const int64_t R = (k.B + nthr - 1) / nthr, ra = (int64_t)t * R, rb = ra + R < k.B ? ra + R : k.B;
-    auto cmark = [&](int64_t r) -> int { return k.skip_zero ? (int)(k.uflags[kMarkB * r] & 1u) : 1; };
-    auto fmark = [&](int64_t r) -> uint32_t { return k.skip_zero ? (uint32_t)(k.uflags[kMarkB * r + 1] & 7u) : 7u; };
-    int sc = 0, sf = 0;
-    for (int64_t r = ra; r < rb; ++r) {
-      sc += cmark(r);
-      sf += __builtin_popcount(fmark(r));
-    }
-    const int ic = (int)wave_incl_sum((double)sc), jf = (int)wave_incl_sum((double)sf);
-    if (lane == 63) {
-      scn[wave] = ic;
-      scn[kB1Waves + wave] = jf;
-    }
-    __syncthreads();
-    int64_t pc = ic - sc, pf = jf - sf;   // this thread's first list positions
-    int nc = 0, nf = 0;                   // the list lengths (made wave-uniform below)
-    for (int q = 0; q < kB1Waves; ++q) {
-      if (q < wave) {
-        pc += scn[q];
-        pf += scn[kB1Waves + q];
-      }
-      nc += scn[q];
-      nf += scn[kB1Waves + q];
-    }
-    const int64_t Nc = __builtin_amdgcn_readfirstlane(nc), Nf = __builtin_amdgcn_readfirstlane(nf);
-    const int G = kB1Waves * (int)nb;
-    int gc = Nc > 0 ? G : 0;                                 // waves on the coarse list
-    if (Nc > 0 && Nf > 0) {
-      gc = (int)((2 * (int64_t)G * Nc + Nc + Nf) / (2 * (Nc + Nf)));
-      gc = gc < 1 ? 1 : (gc > G - 1 ? G - 1 : gc);
-    }
-    if (blockIdx.x == 0 && t == 0) *k.gsplit = gc;
-    int64_t wlo[kB1Waves], whi[kB1Waves];
-    int rounds = 0;
-#pragma unroll
-    for (int w = 0; w < kB1Waves; ++w) {
-      const int g = w * (int)nb + (int)blockIdx.x;
-      const bool fw = g >= gc;
-      const int64_t N = fw ? Nf : Nc;
-      const int gi = fw ? g - gc : g, GG = fw ? G - gc : gc;
-      wlo[w] = GG ? (int64_t)gi * N / GG : 0;
-      whi[w] = GG ? (int64_t)(gi + 1) * N / GG : 0;
-      const int nr = (int)((whi[w] - wlo[w] + kUlCap - 1) / kUlCap);
-      rounds = nr > rounds ? nr : rounds;
-    }
+    // ray order -- coarse tiles, then fine tiles (ray, tile), render_lists_kernel
+    // -- and the kB1Waves x nb MLP waves g = wave * nb + block split them: the
+    // first gsplit waves the coarse list, the others the fine list, in
+    // contiguous slices of equal length (gsplit in proportion to the two
+    // lists).  Every wave then runs ~1/1024 of the work, whatever the scene
+    // leaves nonzero; each wave keeps one net's dW and stores it to slab g,
+    // which the scatter kernel's slab reduction sums in g order:
+    // deterministic (the split is a function of the marks alone).  Tiles, not
+    // the two-tile units of the static split: a live unit often holds a dead
+    // tile.  A wave reads its codes 64 at a time (one vector load; the tile
+    // loop takes them by readlane).
     const int wv = __builtin_amdgcn_readfirstlane(wave);    // wave-uniform (SGPR)
-    const int g_me = wv * (int)nb + (int)blockIdx.x;
+    const int64_t Nc = __builtin_amdgcn_readfirstlane(k.lmeta[0]), Nf = __builtin_amdgcn_readfirstlane(k.lmeta[1]);
+    const int gc = __builtin_amdgcn_readfirstlane(k.lmeta[3]);
+    const int G = kB1Waves * (int)nb, g_me = wv * (int)nb + (int)blockIdx.x;
     const bool fine = g_me >= gc;                            // wave-uniform
+    const int64_t N = fine ? Nf : Nc;
+    const int gi = fine ? g_me - gc : g_me, GG = fine ? G - gc : gc;
+    const int64_t lo = GG ? (int64_t)gi * N / GG : 0, hi = GG ? (int64_t)(gi + 1) * N / GG : 0;
+    const int32_t* L = k.lists + (fine ? 2 * k.B : 0);
     wring_prime(wr, fine ? k.Pf : k.Pc, lane);
-    for (int rd = 0; rd < rounds; ++rd) {
-      // this round's window of each wave's slice: the codes (ray << 3 | fine << 2 | part)
-      int64_t xc = pc, xf = pf;
-      for (int64_t r = ra; r < rb; ++r) {
-        const int cm = cmark(r);
-        const uint32_t fm = fmark(r);
-#pragma unroll
-        for (int w = 0; w < kB1Waves; ++w) {
-          const bool fw = w * (int)nb + (int)blockIdx.x >= gc;
-          const int64_t a = wlo[w] + (int64_t)rd * kUlCap, e = whi[w] < a + kUlCap ? whi[w] : a + kUlCap;
-          if (!fw && cm && xc >= a && xc < e) ul[w * kUlCap + (int)(xc - a)] = (int)(r << 3);
-          if (fw) {
-            int64_t y = xf;
-            for (int part = 0; part < 3; ++part)
-              if ((fm >> part) & 1u) {
-                if (y >= a && y < e) ul[w * kUlCap + (int)(y - a)] = (int)(r << 3) | 4 | part;
-                ++y;
-              }
-          }
-        }
-        xc += cm;
-        xf += __builtin_popcount(fm);
+#ifndef HN_DIAG_NOTILES
+#define HN_DIAG_NOTILES 0   // diagnostic builds: 1 = no tiles
+#endif
+    int prev = -1;   // the ray of this wave's previous tile (its SH set-up is reused)
+    for (int64_t c0 = lo; c0 < (HN_DIAG_NOTILES ? lo : hi); c0 += 64) {
+      const int cnt = (int)(hi - c0 < 64 ? hi - c0 : 64);
+      const int codes = lane < cnt ? L[c0 + lane] : 0;
+      for (int j = 0; j < cnt; ++j) {
+        const int code = __builtin_amdgcn_readlane(codes, j);
+        b1_unit_split(k, (int64_t)(code >> 3), code & 7, fine, X, dw, wr, (code >> 3) != prev);
+        prev = code >> 3;
       }
-      __syncthreads();
-      const int64_t a = wlo[wv] + (int64_t)rd * kUlCap;
-      const int n = __builtin_amdgcn_readfirstlane((int)((whi[wv] < a + kUlCap ? whi[wv] : a + kUlCap) - a));
-      for (int j = 0; j < n; ++j) {
-        const int code = __builtin_amdgcn_readfirstlane(ul[wv * kUlCap + j]);
-        b1_unit_split(k, (int64_t)(code >> 3), code & 3, fine, X, dw, wr);
-      }
-      if (rd + 1 < rounds) __syncthreads();   // the list is rewritten next round
     }
     dw_flush<true>(dw, k.slab + (size_t)g_me * W_END, lane);
   } else {
@@ -3134,7 +3124,7 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4 +
-              ((n * kMarkB / 4 + 1 + 3) & ~(size_t)3);   // + the unit marks (B1K::uflags) and the wave split
+              ((12 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists [11n]
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -3378,8 +3368,9 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
   k.dfeat = dfeat;
   k.draw = draw;
   k.uflags = uflags;
-  // the split schedule's coarse / fine wave split, after the marks
-  k.gsplit = reinterpret_cast<int32_t*>(uflags + kMarkB * (size_t)a->n_rays);
+  // the work lists' counts and the lists, after the marks
+  k.lmeta = reinterpret_cast<int32_t*>(uflags + kMarkB * (size_t)a->n_rays);
+  k.lists = k.lmeta + 8;
   k.ltarget = k.lrgb = k.lrgb0 = k.lsp = k.lsp0 = k.ltv = nullptr;
   k.n_tv = 0;
   k.lgm = k.lsparse = k.lworld = k.lsparse_w = k.ltv_w = 0.f;
@@ -3464,6 +3455,10 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
                      dim3((unsigned)((2 * a->n_rays + kFwdWaves - 1) / kFwdWaves + (k.lout ? 1 : 0))),
                      dim3(64 * kFwdWaves), 0, s, k);
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
+  if (mode == kModeSplit) {   // the backward's work lists (from the pre-pass's marks)
+    hipLaunchKernelGGL(render_lists_kernel, dim3(1), dim3(kListThreads), 0, s, k);
+    if ((st = hip_status(hipGetLastError()))) return st;
+  }
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
   if (mode == kModeSplit)
     hipLaunchKernelGGL((render_bwd_kernel<HN_SW_VMCNT, kModeSplit>), dim3(kBwdBlocks), dim3(64 * kB1Waves), lds, s,
@@ -3483,8 +3478,10 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.draw = draw;
     sk.scramble = k.scramble;
     sk.skip_zero = k.skip_zero;
-    sk.gsplit = k.gsplit;
-    sk.uflags = k.uflags;
+    sk.lmeta = k.lmeta;
+    // the scatter's unit list (each wave holds <= 64 rounds of codes in a register)
+    sk.slist = k.skip_zero && (3 * a->n_rays + kBwdBlocks - 1) / kBwdBlocks <= 64 * kScWaves
+                   ? k.lists + 8 * a->n_rays : nullptr;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
     sk.dfeat_f = k.dfeat_f;
