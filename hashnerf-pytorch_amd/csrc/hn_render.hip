@@ -2530,15 +2530,42 @@ constexpr int kListThreads = 1024;
 __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   __shared__ int tot[3][kListThreads / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t R = (k.B + kListThreads - 1) / kListThreads, ra = (int64_t)t * R;
+  // each thread a run of R rays, R a multiple of 4; up to kRegR of their mark
+  // words are loaded at once (16-byte loads, all in flight: the marks were
+  // written on other XCDs, so each load is a trip past this XCD's L2) and
+  // kept for both passes
+  constexpr int kRegR = 16;
+  const int64_t R = (k.B + 4 * kListThreads - 1) / (4 * kListThreads) * 4, ra = (int64_t)t * R;
   const int64_t rb = ra + R < k.B ? ra + R : k.B;
   // bytes [coarse tiles (2 bits), fine tiles (6), scatter units (3), -]
   auto mword = [&](int64_t r) -> uint32_t {
     return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0x073f03u;
   };
+  uint32_t wreg[kRegR];
+#pragma unroll
+  for (int q = 0; q < kRegR; q += 4) {
+    const int64_t r = ra + q;
+    if (!k.skip_zero || r >= rb || q >= R) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wreg[q + e] = (!k.skip_zero && r + e < rb && q + e < R) ? 0x073f03u : 0u;
+    } else if (r + 4 <= rb) {
+      const uint4 v = *reinterpret_cast<const uint4*>(k.uflags + kMarkB * r);
+      wreg[q] = v.x; wreg[q + 1] = v.y; wreg[q + 2] = v.z; wreg[q + 3] = v.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wreg[q + e] = r + e < rb ? mword(r + e) : 0u;
+    }
+  }
+  auto wat = [&](int64_t r) -> uint32_t {   // the mark word of ray r of this thread's run
+    const int64_t q = r - ra;
+    uint32_t w = 0u;
+#pragma unroll
+    for (int e = 0; e < kRegR; ++e) w = q == e ? wreg[e] : w;
+    return R <= kRegR ? w : mword(r);
+  };
   int nc = 0, nf = 0, ns = 0;
   for (int64_t r = ra; r < rb; ++r) {
-    const uint32_t w = mword(r);
+    const uint32_t w = wat(r);
     nc += __builtin_popcount(w & 3u);
     nf += __builtin_popcount((w >> 8) & 63u);
     ns += __builtin_popcount((w >> 16) & 7u);
@@ -2565,7 +2592,7 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   int32_t* lf = lc + 2 * k.B;
   int32_t* ls = lf + 6 * k.B;
   for (int64_t r = ra; r < rb; ++r) {
-    const uint32_t w = mword(r);
+    const uint32_t w = wat(r);
     for (int i = 0; i < 2; ++i)
       if ((w >> i) & 1u) lc[xc++] = (int32_t)(r << 3) | i;
     for (int i = 0; i < 6; ++i)
