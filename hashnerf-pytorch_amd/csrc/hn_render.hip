@@ -99,11 +99,11 @@ struct B1K {
   float* lout;
   int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
   uint8_t* uflags;      // [B][kMarkB] marks (composite pre-pass): [0] coarse, [1] fine MLP tiles with a
-                        // nonzero d raw, [2] fine units (64 samples) with a nonzero sample or coarse twin
-                        // (the scatter's)
+                        // nonzero d raw, [2] fine tiles with a nonzero sample or coarse twin (the
+                        // scatter's)
   int32_t* lmeta;       // work lists (render_lists_kernel): [0] coarse tiles, [1] fine tiles, [2] scatter
-                        // units, [3] gsplit: the MLP waves g < gsplit run coarse tiles (slab_reduce_block)
-  int32_t* lists;       // coarse tile codes [2B] | fine tile codes [6B] | scatter unit codes [3B]
+                        // tiles, [3] gsplit: the MLP waves g < gsplit run coarse tiles (slab_reduce_block)
+  int32_t* lists;       // coarse tile codes [2B] | fine tile codes [6B] | the scatter's tile codes [6B]
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -1629,7 +1629,7 @@ struct ScK {
   int32_t scramble;       // the MLP backward's ray permutation (B1K::scramble; 0: identity)
   int32_t skip_zero;      // exact-zero skipping (!hn_render_cfg.dense_bwd)
   const int32_t* lmeta;   // render_lists_kernel's counts ([2] scatter units, [3] the MLP waves' split)
-  const int32_t* slist;   // its scatter unit codes (ray << 3 | part), or null: every unit
+  const int32_t* slist;   // its scatter tile codes (ray << 3 | tile), or null: every unit
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
@@ -1738,21 +1738,28 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   bw.cap = (uint32_t)k.bin_cap;
   bw.shift = (uint32_t)k.bin_shift;
   // The block's units.  With exact-zero skipping: its slice of the list of
-  // fine units that have feature grads to scatter (render_lists_kernel, from
+  // fine tiles that have feature grads to scatter (render_lists_kernel, from
   // the composite pre-pass's marks), the list in ray order and cut into equal
   // slices over the blocks -- every block the same share of the work,
-  // whatever the scene leaves nonzero; each wave holds its units' codes in a
-  // register (lane j: round j).  Otherwise (dense_bwd) every unit, the rays
-  // permuted as the MLP backward's (unit_ray).
+  // whatever the scene leaves nonzero; a wave's unit is two consecutive tiles
+  // of the slice, lanes 0-31 the first, 32-63 the second (often of different
+  // rays; the 16-lane run rows never cross them), and each wave holds its
+  // units' codes in registers (lane j: round j).  Otherwise (dense_bwd) every
+  // unit is a third of one ray's fine samples, the rays permuted as the MLP
+  // backward's (unit_ray).
   const bool use_list = k.slist != nullptr;
   int64_t u0 = 0, u1 = 0;
-  int ucode = 0;   // lane j: the code of this wave's unit of round j
+  // lane j: the codes of this wave's two tiles of round j (-1: none)
+  int ucode0 = -1, ucode1 = -1;
   if (use_list) {
     const int64_t Ns = __builtin_amdgcn_readfirstlane(k.lmeta[2]);
     const int64_t s0 = (int64_t)blockIdx.x * Ns / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * Ns / gridDim.x;
-    u1 = s1 - s0;
+    u1 = (s1 - s0 + 1) / 2;   // a unit = two consecutive tiles of the slice, one per lane half
     const int64_t uj = wave + (int64_t)lane * kScWaves;
-    if (lane < 64 && uj < u1) ucode = k.slist[s0 + uj];
+    if (uj < u1) {
+      ucode0 = k.slist[s0 + 2 * uj];
+      if (s0 + 2 * uj + 1 < s1) ucode1 = k.slist[s0 + 2 * uj + 1];
+    }
   } else {
     const int64_t units = 3 * k.B;
     const int64_t per = (units + gridDim.x - 1) / gridDim.x;
@@ -1837,10 +1844,27 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
     q.g0 = q.g1 = 0.f;
     q.tb = q.tw = nullptr;
     if (q.act) {
-      const int code = use_list ? __builtin_amdgcn_readlane(ucode, (int)it) : 0;
-      const int64_t ray = use_list ? (int64_t)(code >> 3) : unit_ray(u / 3);
-      const int i = 64 * (use_list ? (code & 3) : (int)(u % 3)) + lane;   // fine sample
-      load_ray(k.rays, ray, q.r);
+      int64_t ray;
+      int i;   // the lane's fine sample
+      bool none = false;   // a second tile that does not exist: no grads
+      if (use_list) {
+        const int ca = __builtin_amdgcn_readlane(ucode0, (int)it), cb = __builtin_amdgcn_readlane(ucode1, (int)it);
+        none = lane >= 32 && cb < 0;
+        const int code = lane < 32 || cb < 0 ? ca : cb;
+        ray = code >> 3;
+        i = 32 * (code & 7) + (lane & 31);
+      } else {
+        ray = unit_ray(u / 3);
+        i = 64 * (int)(u % 3) + lane;
+      }
+      {
+        const float* rb = k.rays + 11 * ray;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          q.r.o[a] = rb[a];
+          q.r.d[a] = rb[3 + a];
+        }
+      }
       ray_point(q.r, k.z_fine[ray * kSf + i], q.pt);
 #pragma unroll
       for (int a = 0; a < 3; ++a) q.xc[a] = clamp_t(q.pt[a], k.g.bmin[a], k.g.bmax[a]);
@@ -1849,10 +1873,10 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       // MLP backward did not store them: b1_unit_split's skip); the same for
       // its coarse twin
       const float* dr = k.draw + (size_t)ray * (kSc + kSf) * 4;
-      if (!k.skip_zero || draw_nonzero(*reinterpret_cast<const float4*>(dr + 4 * (kSc + i))))
+      if (!none && (!k.skip_zero || draw_nonzero(*reinterpret_cast<const float4*>(dr + 4 * (kSc + i)))))
         q.tb = k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024 + 4 * (i & 31);
       const int src = k.fine_src[ray * kSf + i];
-      if (src < kSc && (!k.skip_zero || draw_nonzero(*reinterpret_cast<const float4*>(dr + 4 * src))))
+      if (!none && src < kSc && (!k.skip_zero || draw_nonzero(*reinterpret_cast<const float4*>(dr + 4 * src))))
         q.tw = k.dfeat_c + (size_t)ray * kDcRay + (size_t)(src >> 5) * 1024 + 4 * (src & 31);
       // no lane with a gradient: the unit writes no record (wave-uniform)
       q.act = __ballot(q.tb != nullptr || q.tw != nullptr) != 0ull;
@@ -2441,16 +2465,18 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   }
   __syncthreads();
   if (active && fine) {
-    // the scatter's marks: bit u = a sample of fine unit u, or its coarse twin
-    // (the same point, fine_src < 64), has a nonzero d raw -- the unit has
-    // feature grads to scatter (scatter_bins_kernel's unit lists)
+    // the scatter's marks: bit t = a sample of fine tile t, or its coarse twin
+    // (the same point, fine_src < 64), has a nonzero d raw -- the tile has
+    // feature grads to scatter (scatter_bins_kernel's lists)
     const unsigned long long cm = cmask[wave >> 1];
-    uint32_t su = 0u;
+    uint32_t su = 0u;   // bit t: fine tile t (32 samples) has feature grads to scatter
     for (int j = lane; j < kSf; j += 64) {
       const int src = k.fine_src[ray * kSf + j];
       const bool nz = draw_nonzero(*reinterpret_cast<const float4*>(rawb + 4 * j)) ||
                       (src < kSc && ((cm >> src) & 1ull) != 0ull);
-      su |= (__ballot(nz) != 0ull ? 1u : 0u) << (j >> 6);
+      const uint64_t b = __ballot(nz);
+      su |= ((uint32_t)b != 0u ? 1u : 0u) << (2 * (j >> 6));
+      su |= ((uint32_t)(b >> 32) != 0u ? 1u : 0u) << (2 * (j >> 6) + 1);
     }
     if (lane == 0) k.uflags[kMarkB * ray + 2] = (uint8_t)su;
   }
@@ -2519,10 +2545,10 @@ HN_DEV void dw_zero(DW& dw) {
 }
 
 // The backward's work lists (round 6), from the composite pre-pass's marks
-// (B1K::uflags; every tile and unit with dense_bwd): the coarse tiles, the
-// fine tiles and the scatter's fine units with feature grads, each in ray
-// order, as codes (ray << 3 | tile or part); their lengths and the MLP
-// waves' coarse / fine split.  One 1024-thread workgroup: each thread a run
+// (B1K::uflags; every tile with dense_bwd): the coarse tiles, the fine tiles
+// and the scatter's fine tiles with feature grads, each in ray order, as
+// codes (ray << 3 | tile); their lengths and the MLP waves' coarse / fine
+// split.  One 1024-thread workgroup: each thread a run
 // of rays, a block-wide prefix of its counts, then its codes.  (Computed
 // redundantly by every block of the two kernels that use them it cost the
 // MLP backward ~28 us.)
@@ -2537,9 +2563,9 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   constexpr int kRegR = 16;
   const int64_t R = (k.B + 4 * kListThreads - 1) / (4 * kListThreads) * 4, ra = (int64_t)t * R;
   const int64_t rb = ra + R < k.B ? ra + R : k.B;
-  // bytes [coarse tiles (2 bits), fine tiles (6), scatter units (3), -]
+  // bytes [coarse tiles (2 bits), fine tiles (6), the scatter's fine tiles (6), -]
   auto mword = [&](int64_t r) -> uint32_t {
-    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0x073f03u;
+    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0x3f3f03u;
   };
   uint32_t wreg[kRegR];
 #pragma unroll
@@ -2547,7 +2573,7 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
     const int64_t r = ra + q;
     if (!k.skip_zero || r >= rb || q >= R) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) wreg[q + e] = (!k.skip_zero && r + e < rb && q + e < R) ? 0x073f03u : 0u;
+      for (int e = 0; e < 4; ++e) wreg[q + e] = (!k.skip_zero && r + e < rb && q + e < R) ? 0x3f3f03u : 0u;
     } else if (r + 4 <= rb) {
       const uint4 v = *reinterpret_cast<const uint4*>(k.uflags + kMarkB * r);
       wreg[q] = v.x; wreg[q + 1] = v.y; wreg[q + 2] = v.z; wreg[q + 3] = v.w;
@@ -2568,7 +2594,7 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
     const uint32_t w = wat(r);
     nc += __builtin_popcount(w & 3u);
     nf += __builtin_popcount((w >> 8) & 63u);
-    ns += __builtin_popcount((w >> 16) & 7u);
+    ns += __builtin_popcount((w >> 16) & 63u);
   }
   const int ic = (int)wave_incl_sum((double)nc), jf = (int)wave_incl_sum((double)nf), ks = (int)wave_incl_sum((double)ns);
   if (lane == 63) {
@@ -2597,7 +2623,7 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
       if ((w >> i) & 1u) lc[xc++] = (int32_t)(r << 3) | i;
     for (int i = 0; i < 6; ++i)
       if ((w >> (8 + i)) & 1u) lf[xf++] = (int32_t)(r << 3) | i;
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 6; ++i)
       if ((w >> (16 + i)) & 1u) ls[xs++] = (int32_t)(r << 3) | i;
   }
   if (t == 0) {
@@ -3151,7 +3177,7 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4 +
-              ((12 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists [11n]
+              ((15 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists [14n]
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -3507,7 +3533,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.skip_zero = k.skip_zero;
     sk.lmeta = k.lmeta;
     // the scatter's unit list (each wave holds <= 64 rounds of codes in a register)
-    sk.slist = k.skip_zero && (3 * a->n_rays + kBwdBlocks - 1) / kBwdBlocks <= 64 * kScWaves
+    sk.slist = k.skip_zero && (6 * a->n_rays + kBwdBlocks - 1) / kBwdBlocks <= 2 * 64 * kScWaves
                    ? k.lists + 8 * a->n_rays : nullptr;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
