@@ -89,8 +89,25 @@ HN_DEV int32_t cell_floor(float num, float g, float rg) {
   const float r = __builtin_fmaf(-g, q0, num);
   return (int32_t)floorf(__builtin_fmaf(r, rg, q0));
 }
+// n / d, correctly rounded, for operands the division's scaling never
+// touches (|n|, |d| well inside [2^-96, 2^96], d != 0, finite): the FMA
+// sequence hipcc emits for an IEEE f32 division (rcp, two refinements, the
+// final residual correction) without its v_div_scale pair and v_div_fixup,
+// which leave such operands unchanged -- the same bits in 8 instructions
+// instead of 11.  The trilinear weights (x - vmin) / (vmax - vmin): grid
+// sizes and sample coordinates of a NeRF scene are far inside that range.
+HN_DEV float div_rn(float n, float d) {
+  float y = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, y, 1.f);
+  y = __builtin_fmaf(e, y, y);
+  float q = n * y;
+  const float r = __builtin_fmaf(-d, q, n);
+  q = __builtin_fmaf(r, y, q);
+  const float r2 = __builtin_fmaf(-d, q, n);
+  return __builtin_fmaf(r2, y, q);
+}
 // voxel_level with the cells from cell_floor (rg[a] = RN(1/gs[a])); the
-// weights keep the reference's IEEE divisions.
+// weights keep the reference's IEEE divisions (div_rn: the same bits).
 HN_DEV void voxel_level_rcp(const float x[3], const float xc[3], const float gs[3], const float rg[3],
                             const float bmin[3], uint32_t mask, Voxel& v) {
   uint32_t c[3];
@@ -99,7 +116,7 @@ HN_DEV void voxel_level_rcp(const float x[3], const float xc[3], const float gs[
     const int32_t i = cell_floor(xc[a] - bmin[a], gs[a], rg[a]);   // floor((x - min) / g).int()
     const float vmin = (float)i * gs[a] + bmin[a];
     const float vmax = vmin + gs[a];
-    v.w[a] = (x[a] - vmin) / (vmax - vmin);
+    v.w[a] = div_rn(x[a] - vmin, vmax - vmin);
     c[a] = (uint32_t)i;
   }
   const uint32_t x0 = c[0], x1 = c[0] + 1u;

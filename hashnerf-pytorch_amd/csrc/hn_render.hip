@@ -1523,7 +1523,7 @@ HN_DEV void voxel_cw_sc(const GridArgs& g, const float* gsl, const float pt[3], 
     const int32_t i = cell_floor(xc[a] - g.bmin[a], gs, gsl[kGsRcp + 3 * l + a]);
     const float vmin = (float)i * gs + g.bmin[a];
     const float vmax = vmin + gs;
-    w[a] = (pt[a] - vmin) / (vmax - vmin);
+    w[a] = div_rn(pt[a] - vmin, vmax - vmin);
     cell[a] = i;
   }
 }
