@@ -3049,6 +3049,52 @@ __global__ __launch_bounds__(kBinThreads) void bin_reduce_kernel(BinR k) {
   __syncthreads();
   const double inv = 1.0 / (double)scale;
   float4* dst = k.d_table ? reinterpret_cast<float4*>(k.d_table + e0) : nullptr;
+  if (k.fused && dst == nullptr) {
+    // fused step: the thread's live flags, then all of its p, m, v loads in
+    // flight at once (one HBM round trip instead of one per float4: the
+    // pass 90.5 -> 88.6 us on config 2)
+    bool lv[kSliceF4];
+#pragma unroll
+    for (int j = 0; j < kSliceF4; ++j) {
+      const int i = threadIdx.x + j * kBinThreads;
+      lv[j] = i < nd4 && live_at(i);
+    }
+    f32x4 p4[kSliceF4], m4[kSliceF4], v4[kSliceF4];
+#pragma unroll
+    for (int j = 0; j < kSliceF4; ++j) {
+      const int i = threadIdx.x + j * kBinThreads;
+      if (lv[j]) {
+        p4[j] = reinterpret_cast<const f32x4*>(k.step.p + e0)[i];
+        m4[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(k.step.m + e0) + i);
+        v4[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(k.step.v + e0) + i);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kSliceF4; ++j) {
+      const int i = threadIdx.x + j * kBinThreads;
+      if (i >= nd4) break;
+      float4 a;
+      a.x = (float)((double)(long long)acc[2 * i] * inv);
+      a.y = (float)((double)(long long)acc[se + 2 * i] * inv);
+      a.z = (float)((double)(long long)acc[2 * i + 1] * inv);
+      a.w = (float)((double)(long long)acc[se + 2 * i + 1] * inv);
+      if (!lv[j]) {
+        if (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f)
+          __hip_atomic_fetch_or(&g_hn_fault, kFaultDeadRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
+      float4 p{p4[j][0], p4[j][1], p4[j][2], p4[j][3]}, m{m4[j][0], m4[j][1], m4[j][2], m4[j][3]},
+          v{v4[j][0], v4[j][1], v4[j][2], v4[j][3]};
+      radam_elem(k.step, p.x, a.x, m.x, v.x);
+      radam_elem(k.step, p.y, a.y, m.y, v.y);
+      radam_elem(k.step, p.z, a.z, m.z, v.z);
+      radam_elem(k.step, p.w, a.w, m.w, v.w);
+      __builtin_nontemporal_store(f32x4{m.x, m.y, m.z, m.w}, reinterpret_cast<f32x4*>(k.step.m + e0) + i);
+      __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(k.step.v + e0) + i);
+      if (k.step.mode != 0) reinterpret_cast<f32x4*>(k.step.p + e0)[i] = f32x4{p.x, p.y, p.z, p.w};
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < kSliceF4; ++j) {   // entries 2i, 2i + 1
     const int i = threadIdx.x + j * kBinThreads;
