@@ -121,12 +121,16 @@ HN_DEV void ring_fill(const float* P, float* slot, int off, int lane) {
   asm volatile("" : "+s"(so));
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(opaque_ptr(P)), (short)0, 0x7fffffff, 0x00020000);
+#ifndef HN_DIAG_RING2
+#define HN_DIAG_RING2 0
+#endif
 #pragma unroll
-  for (int q = 0; q < 3; ++q)
+  for (int q = 0; q < (HN_DIAG_RING2 ? 2 : 3); ++q)   // HN_DIAG_RING2: timing diagnostic only (stale third part)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + 256 * q), 16,
                                              lane * 16, so + 1024 * q, 0, 0);
 }
 HN_DEV void fwd_ring_start(const float* P, float* slot, int lane) {
+  if (HN_DIAG_RING2) *reinterpret_cast<f32x4*>(slot + 512 + 4 * lane) = f32x4{0.f, 0.f, 0.f, 0.f};
   ring_fill(P, slot, fwd_chunk_off(kFwdSeq[0]), lane);
 }
 template <int R, typename BF, typename Src>
