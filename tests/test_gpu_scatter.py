@@ -35,7 +35,7 @@ def _rel(a, b):
     return float(torch.linalg.norm(a - b) / max(float(torch.linalg.norm(b)), 1e-30))
 
 
-def _state(hn, B, T, seed, scatter, bin_cap=0, box=BOX, finest=512):
+def _state(hn, B, T, seed, scatter, bin_cap=0, box=BOX, finest=512, sigma_sign=0):
     from importlib import import_module
     HF = import_module("hashnerf_pytorch_amd.functional")
     torch.manual_seed(seed)
@@ -45,6 +45,11 @@ def _state(hn, B, T, seed, scatter, bin_cap=0, box=BOX, finest=512):
     kw = dict(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3, hidden_dim_color=64,
               input_ch=32, input_ch_views=16)
     mc, mf = hn.NeRFSmall(**kw).to(DEV), hn.NeRFSmall(**kw).to(DEV)
+    if sigma_sign:   # sigma = w . relu(h): all weights of one sign fix the sign of every raw sigma
+        with torch.no_grad():
+            for m in (mc, mf):
+                w = m.sigma_net[1].weight
+                w[0] = sigma_sign * w[0].abs()
     focal, K = hn.rays.blender_intrinsics(400, 400)
     ro, rd = hn.get_rays(400, 400, K, hn.pose_spherical(30.0 + seed, -30.0, 4.0)[:3, :4].to(DEV))
     sel = torch.randperm(400 * 400, device=DEV)[:B]
@@ -483,3 +488,37 @@ def test_fine_z_sort_structure(hn, perturb):
     prev = torch.cat([torch.full((zf.shape[0], 1), -1.0), zf[:, :-1]], 1)
     prev_tag = torch.cat([torch.zeros((zf.shape[0], 1), dtype=torch.long), src[:, :-1]], 1)
     assert not ((prev == zf) & coarse & (prev_tag == 255)).any()
+
+
+@pytest.mark.parametrize("sign", [-1, 1])
+def test_skip_extremes_match_dense(hn, sign):
+    """Exact-zero skipping at its two ends (ABI 14 hn_render_cfg.dense_bwd):
+    every raw sigma <= 0 (sign -1: no sample has a weight, every d raw is 0,
+    the work lists are empty) and every raw sigma >= 0 (sign +1: nearly
+    nothing to skip).  The skipping backward equals the dense one: the table
+    gradient bitwise (exact integer sums), the ten NeRFSmall gradients within
+    1e-5 (per-wave grouping), all exact zeros for sign -1; no device fault."""
+    HF, emb, mc, mf, ws, rays, t_rand, u, target, st, grads = _state(hn, 1024, 16, 23, "binned",
+                                                                     sigma_sign=sign)
+    sig = torch.cat([st.raw_c[..., 3].reshape(-1), st.raw_f[..., 3].reshape(-1)])
+    if sign < 0:
+        assert bool((sig <= 0).all())
+    else:
+        assert float((sig > 0).float().mean()) > 0.9
+    res = {}
+    for dense in (1, 0):
+        st.cfg.dense_bwd = dense
+        res[dense] = _bwd(HF, emb, ws, st, grads)
+    st.cfg.dense_bwd = 0
+    (td, wd), (ts, wsk) = res[1], res[0]
+    assert torch.equal(td + 0.0, ts + 0.0), "table gradient: skipping changed it"
+    for k, (a, b) in enumerate(zip(wd, wsk)):
+        if sign < 0:
+            assert torch.count_nonzero(a) == 0 and torch.count_nonzero(b) == 0, f"gradient {k} not zero"
+        else:
+            rel = float((a.double() - b.double()).norm() / a.double().norm().clamp_min(1e-30))
+            assert rel <= 1e-5, f"gradient {k}: skipped vs dense relative {rel:.3e}"
+    if sign < 0:
+        assert torch.count_nonzero(ts) == 0
+    else:
+        assert torch.count_nonzero(ts) > 0
