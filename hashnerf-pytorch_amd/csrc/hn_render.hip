@@ -2548,85 +2548,78 @@ HN_DEV void dw_zero(DW& dw) {
 // (B1K::uflags; every tile with dense_bwd): the coarse tiles, the fine tiles
 // and the scatter's fine tiles with feature grads, each in ray order, as
 // codes (ray << 3 | tile); their lengths and the MLP waves' coarse / fine
-// split.  One 1024-thread workgroup: each thread a run
-// of rays, a block-wide prefix of its counts, then its codes.  (Computed
-// redundantly by every block of the two kernels that use them it cost the
-// MLP backward ~28 us.)
-constexpr int kListThreads = 1024;
+// split.  Workgroup w writes the codes of rays [w R, (w + 1) R): it counts
+// the marks of every earlier ray itself (a few loads per thread; no
+// workgroup waits for another), then takes 256 rays at a time, one per
+// thread, with a block-wide prefix of their counts.  (One 1,024-thread
+// workgroup for the whole batch took 14 us; computed redundantly by every
+// block of the kernels that use the lists it cost the MLP backward ~28 us.)
+constexpr int kListThreads = 256;
+constexpr int kListMaxBlocks = 64;
+HN_DEV int list_block_scan(int v, int* sh) {   // inclusive scan over the workgroup; sh: 4 ints of LDS
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  __syncthreads();   // sh free (its previous use is complete)
+  if (lane == 63) sh[wave] = v;
+  __syncthreads();
+  for (int q = 0; q < wave; ++q) v += sh[q];
+  return v;
+}
+HN_DEV int list_block_sum(int v, int* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
 __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
-  __shared__ int tot[3][kListThreads / 64];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  // each thread a run of R rays, R a multiple of 4; up to kRegR of their mark
-  // words are loaded at once (16-byte loads, all in flight: the marks were
-  // written on other XCDs, so each load is a trip past this XCD's L2) and
-  // kept for both passes
-  constexpr int kRegR = 16;
-  const int64_t R = (k.B + 4 * kListThreads - 1) / (4 * kListThreads) * 4, ra = (int64_t)t * R;
-  const int64_t rb = ra + R < k.B ? ra + R : k.B;
+  static_assert(kListThreads == 256, "list_block_scan: 4 waves");
+  __shared__ int sh[3][4];
+  const int t = threadIdx.x;
   // bytes [coarse tiles (2 bits), fine tiles (6), the scatter's fine tiles (6), -]
   auto mword = [&](int64_t r) -> uint32_t {
     return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0x3f3f03u;
   };
-  uint32_t wreg[kRegR];
-#pragma unroll
-  for (int q = 0; q < kRegR; q += 4) {
-    const int64_t r = ra + q;
-    if (!k.skip_zero || r >= rb || q >= R) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wreg[q + e] = (!k.skip_zero && r + e < rb && q + e < R) ? 0x3f3f03u : 0u;
-    } else if (r + 4 <= rb) {
-      const uint4 v = *reinterpret_cast<const uint4*>(k.uflags + kMarkB * r);
-      wreg[q] = v.x; wreg[q + 1] = v.y; wreg[q + 2] = v.z; wreg[q + 3] = v.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wreg[q + e] = r + e < rb ? mword(r + e) : 0u;
-    }
+  const int64_t R = (k.B + gridDim.x - 1) / gridDim.x;
+  const int64_t ra = (int64_t)blockIdx.x * R, rb = ra + R < k.B ? ra + R : k.B;
+  // the counts of the rays before this workgroup's range, and of all rays
+  int bc = 0, bf = 0, bs = 0, tc = 0, tf = 0, ts = 0;
+  for (int64_t r = t; r < k.B; r += kListThreads) {
+    const uint32_t w = mword(r);
+    const int c = __builtin_popcount(w & 3u), f = __builtin_popcount((w >> 8) & 63u),
+              g = __builtin_popcount((w >> 16) & 63u);
+    tc += c; tf += f; ts += g;
+    if (r < ra) { bc += c; bf += f; bs += g; }
   }
-  auto wat = [&](int64_t r) -> uint32_t {   // the mark word of ray r of this thread's run
-    const int64_t q = r - ra;
-    uint32_t w = 0u;
-#pragma unroll
-    for (int e = 0; e < kRegR; ++e) w = q == e ? wreg[e] : w;
-    return R <= kRegR ? w : mword(r);
-  };
-  int nc = 0, nf = 0, ns = 0;
-  for (int64_t r = ra; r < rb; ++r) {
-    const uint32_t w = wat(r);
-    nc += __builtin_popcount(w & 3u);
-    nf += __builtin_popcount((w >> 8) & 63u);
-    ns += __builtin_popcount((w >> 16) & 63u);
-  }
-  const int ic = (int)wave_incl_sum((double)nc), jf = (int)wave_incl_sum((double)nf), ks = (int)wave_incl_sum((double)ns);
-  if (lane == 63) {
-    tot[0][wave] = ic;
-    tot[1][wave] = jf;
-    tot[2][wave] = ks;
-  }
-  __syncthreads();
-  int64_t xc = ic - nc, xf = jf - nf, xs = ks - ns, Nc = 0, Nf = 0, Ns = 0;
-  for (int q = 0; q < kListThreads / 64; ++q) {
-    if (q < wave) {
-      xc += tot[0][q];
-      xf += tot[1][q];
-      xs += tot[2][q];
-    }
-    Nc += tot[0][q];
-    Nf += tot[1][q];
-    Ns += tot[2][q];
-  }
+  int64_t xc = list_block_sum(bc, sh[0]), xf = list_block_sum(bf, sh[1]), xs = list_block_sum(bs, sh[2]);
+  const int64_t Nc = list_block_sum(tc, sh[0]), Nf = list_block_sum(tf, sh[1]), Ns = list_block_sum(ts, sh[2]);
   int32_t* lc = k.lists;
   int32_t* lf = lc + 2 * k.B;
   int32_t* ls = lf + 6 * k.B;
-  for (int64_t r = ra; r < rb; ++r) {
-    const uint32_t w = wat(r);
+  for (int64_t r0 = ra; r0 < rb; r0 += kListThreads) {
+    const int64_t r = r0 + t;
+    const uint32_t w = r < rb ? mword(r) : 0u;
+    const int c = __builtin_popcount(w & 3u), f = __builtin_popcount((w >> 8) & 63u),
+              g = __builtin_popcount((w >> 16) & 63u);
+    const int ic = list_block_scan(c, sh[0]), jf = list_block_scan(f, sh[1]), ks = list_block_scan(g, sh[2]);
+    int64_t oc = xc + ic - c, of = xf + jf - f, os = xs + ks - g;
     for (int i = 0; i < 2; ++i)
-      if ((w >> i) & 1u) lc[xc++] = (int32_t)(r << 3) | i;
+      if ((w >> i) & 1u) lc[oc++] = (int32_t)(r << 3) | i;
     for (int i = 0; i < 6; ++i)
-      if ((w >> (8 + i)) & 1u) lf[xf++] = (int32_t)(r << 3) | i;
+      if ((w >> (8 + i)) & 1u) lf[of++] = (int32_t)(r << 3) | i;
     for (int i = 0; i < 6; ++i)
-      if ((w >> (16 + i)) & 1u) ls[xs++] = (int32_t)(r << 3) | i;
+      if ((w >> (16 + i)) & 1u) ls[os++] = (int32_t)(r << 3) | i;
+    xc += list_block_sum(c, sh[0]);
+    xf += list_block_sum(f, sh[1]);
+    xs += list_block_sum(g, sh[2]);
   }
-  if (t == 0) {
+  if (blockIdx.x == 0 && t == 0) {
     const int G = kB1Waves * kBwdBlocks;
     int gc = Nc > 0 ? G : 0;   // MLP waves on the coarse list, in proportion to the lists
     if (Nc > 0 && Nf > 0) {
@@ -3555,7 +3548,9 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
                      dim3(64 * kFwdWaves), 0, s, k);
   const size_t lds = (size_t)kB1LdsF * sizeof(float);
   if (mode == kModeSplit) {   // the backward's work lists (from the pre-pass's marks)
-    hipLaunchKernelGGL(render_lists_kernel, dim3(1), dim3(kListThreads), 0, s, k);
+    const int64_t nlb = (a->n_rays + kListThreads - 1) / kListThreads;
+    hipLaunchKernelGGL(render_lists_kernel, dim3((unsigned)(nlb < kListMaxBlocks ? nlb : kListMaxBlocks)),
+                       dim3(kListThreads), 0, s, k);
     if ((st = hip_status(hipGetLastError()))) return st;
   }
   // 16 levels x 2^T x 8 B >= 256 MiB from T = 21: the table no longer fits the MALL
