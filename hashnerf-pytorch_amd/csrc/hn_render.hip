@@ -44,6 +44,9 @@ constexpr int kEncGroup = 2;
 constexpr int kSc = 64, kNi = 128, kSf = 192;
 constexpr int kFwdWaves = 4;
 constexpr int kBwdBlocks = 256;          // persistent backward: one block per CU
+#ifndef HN_DW_BLOCKRED   // the MLP backward's dW summed per block before the slab store (render_bwd_kernel)
+#define HN_DW_BLOCKRED 1
+#endif
 
 struct RenderK {
   GridArgs g;
@@ -1567,8 +1570,15 @@ HN_DEV void slab_reduce_block(const float* __restrict__ slab, int n_blocks, cons
   // 0 (coarse) or 1..3 (fine), flattened
   const int gs = gsplit ? *gsplit : 0;
   const int per = fine ? kSlabSlots - 1 : 1;
-  const int n_slabs = gsplit ? (fine ? kSlabSlots * n_blocks - gs : gs) : n_blocks * per;
+  // HN_DW_BLOCKRED: only each block's run leaders hold a slab -- coarse: the
+  // waves 4j < gs; fine: gs, then the waves 4j > gs
+  const int n_lead = fine ? (kSlabSlots * n_blocks) / 4 - gs / 4 : (gs + 3) / 4;
+  const int n_slabs = gsplit ? (HN_DW_BLOCKRED ? n_lead : (fine ? kSlabSlots * n_blocks - gs : gs)) : n_blocks * per;
   auto slab_at = [&](int q) {
+    if (gsplit && HN_DW_BLOCKRED) {
+      const int g = !fine ? 4 * q : (gs % 4 == 0 ? gs + 4 * q : (q == 0 ? gs : 4 * (gs / 4 + q)));
+      return slab[(size_t)g * W_END + i];
+    }
     if (gsplit) return slab[(size_t)(fine ? gs + q : q) * W_END + i];
     const int b = q / per, slot = fine ? 1 + q % per : 0;
     return slab[((size_t)b * kSlabSlots + slot) * W_END + i];
@@ -2544,6 +2554,40 @@ HN_DEV void dw_zero(DW& dw) {
   for (int j = 0; j < 4; ++j) dw.c1[j] = zero16();
 }
 
+// The block's MLP waves sum their dW before the slab store (HN_DW_BLOCKRED):
+// a wave's 12 accumulator blocks through LDS as [block][quad][lane] f32x4
+// (48 KiB; conflict-free b128 accesses), added by the first wave of the block
+// that runs the same net, in wave order.
+template <typename F>
+HN_DEV void dw_each(DW& dw, F&& f) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) f(dw.c2[j], j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f(dw.c1[j], 2 + j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) f(dw.c0[j], 6 + j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) f(dw.s1[j], 8 + j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) f(dw.s0[j], 10 + j);
+}
+HN_DEV void dw_to_lds(DW& dw, f32x4* L, int lane) {
+  dw_each(dw, [&](f32x16& v, int b) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) L[(b * 4 + q) * 64 + lane] = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+  });
+}
+HN_DEV void dw_add_lds(DW& dw, const f32x4* L, int lane) {
+  dw_each(dw, [&](f32x16& v, int b) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 t = L[(b * 4 + q) * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * q + j] = v[4 * q + j] + t[j];
+    }
+  });
+}
+
 // The backward's work lists (round 6), from the composite pre-pass's marks
 // (B1K::uflags; every tile with dense_bwd): the coarse tiles, the fine tiles
 // and the scatter's fine tiles with feature grads, each in ray order, as
@@ -2702,7 +2746,9 @@ void render_bwd_kernel(B1K k) {
     const int wv = __builtin_amdgcn_readfirstlane(wave);    // wave-uniform (SGPR)
     const int64_t Nc = __builtin_amdgcn_readfirstlane(k.lmeta[0]), Nf = __builtin_amdgcn_readfirstlane(k.lmeta[1]);
     const int gc = __builtin_amdgcn_readfirstlane(k.lmeta[3]);
-    const int G = kB1Waves * (int)nb, g_me = wv * (int)nb + (int)blockIdx.x;
+    static_assert(kB1Waves == 4 && kSlabSlots == kB1Waves, "slab_reduce_block's run leaders: 4 waves per block");
+    const int G = kB1Waves * (int)nb,
+              g_me = HN_DW_BLOCKRED ? (int)blockIdx.x * kB1Waves + wv : wv * (int)nb + (int)blockIdx.x;
     const bool fine = g_me >= gc;                            // wave-uniform
     const int64_t N = fine ? Nf : Nc;
     const int gi = fine ? g_me - gc : g_me, GG = fine ? G - gc : gc;
@@ -2722,7 +2768,26 @@ void render_bwd_kernel(B1K k) {
         prev = code >> 3;
       }
     }
-    dw_flush<true>(dw, k.slab + (size_t)g_me * W_END, lane);
+    if (HN_DW_BLOCKRED) {
+      // the block's waves g0 .. g0 + 3 run the coarse net below gc, the fine
+      // one from gc: each run of same-net waves is summed into its first wave
+      // (wave order), which alone stores a slab (slab_reduce_block's leaders)
+      const int g0 = (int)blockIdx.x * kB1Waves;
+      f32x4* red = smem4;
+      for (int w = 1; w < kB1Waves; ++w) {
+        const bool w_leads = g0 + w == gc;                  // first fine wave of the block
+        int ldr = 0;                                        // the leader of wave w
+        if (g0 + w >= gc && g0 < gc) ldr = gc - g0;         // a fine wave behind the block's coarse ones
+        __syncthreads();
+        if (!w_leads && wv == w) dw_to_lds(dw, red, lane);
+        __syncthreads();
+        if (!w_leads && wv == ldr) dw_add_lds(dw, red, lane);
+      }
+      const bool leader = wv == 0 || g_me == gc;
+      if (leader) dw_flush<true>(dw, k.slab + (size_t)g_me * W_END, lane);
+    } else {
+      dw_flush<true>(dw, k.slab + (size_t)g_me * W_END, lane);
+    }
   } else {
     if (wave == 0) {
       wring_prime(wr, k.Pc, lane);
