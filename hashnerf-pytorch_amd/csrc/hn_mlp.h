@@ -220,17 +220,20 @@ HN_DEV void mask16(f32x16& g, const f32x16& act) {   // relu backward (result > 
 // activation live until then -- that spilled the render forward 39 -> 158).
 // C0Init(ob): color_net.0's SH half for output block ob (constant along a ray:
 // the fused forward computes it once per ray and seeds every tile with it).
-template <bool MASKS = false, typename C0Init, typename Src>
+struct NoLive {
+  HN_DEV void operator()() const {}
+};
+template <bool MASKS = false, typename C0Init, typename Src, typename OnLive = NoLive>
 HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, MlpAct& a, f32x16& c2,
-                             int lane, bool skip_dead = false);
+                             int lane, bool skip_dead = false, OnLive&& on_live = OnLive{});
 template <bool MASKS = false, typename C0Init>
 HN_DEV void mlp_fwd_tile_c0(const float* __restrict__ P, const f32x16& feat, C0Init&& c0init,
                             MlpAct& a, f32x16& c2, int lane) {
   mlp_fwd_tile_src<MASKS>(FragGlobal{P}, feat, c0init, a, c2, lane);
 }
-template <bool MASKS, typename C0Init, typename Src>
+template <bool MASKS, typename C0Init, typename Src, typename OnLive>
 HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, MlpAct& a, f32x16& c2,
-                             int lane, bool skip_dead) {
+                             int lane, bool skip_dead, OnLive&& on_live) {
   a.m[0] = a.m[1] = a.m[2] = 0u;
   // sigma_net.0: 32 -> 64, ReLU
   // (Both output blocks of a GEMM sharing one B split per chunk, as the
@@ -259,6 +262,7 @@ HN_DEV void mlp_fwd_tile_src(const Src& P, const f32x16& feat, C0Init&& c0init, 
     }
     return;
   }
+  on_live();   // the tile has density (or nothing is skipped): e.g. its features are stored
   // color_net.0: [sh16 | geo15] -> 64, ReLU
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {

@@ -40,6 +40,9 @@ namespace hn {
 // levels per scheduling group of the forward's encode (8 gathers each):
 // 1 level 0.2674, 2 levels 0.2666, 4 levels 0.2696 ms (r04z)
 constexpr int kEncGroup = 2;
+#ifndef HN_FWD_SKIP_STORES
+#define HN_FWD_SKIP_STORES 1
+#endif
 
 constexpr int kSc = 64, kNi = 128, kSf = 192;
 constexpr int kFwdWaves = 4;
@@ -434,12 +437,20 @@ void render_fwd_kernel(RenderK k) {
       }
     }
     HN_FT_FEAT(3, feat);
-    if (k.feat) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat, k.feat_nt != 0);
     MlpAct a;
     f32x16 c2;
+    // skip_dead: a fine tile without density has no nonzero d raw, so the
+    // backward (dense_bwd = 0: its work lists) never reads its features or
+    // masks -- they are not stored (HN_FWD_SKIP_STORES)
+    const bool dead_skip = k.skip_dead && k.noise_f == nullptr;
+    bool stored = !HN_FWD_SKIP_STORES || !dead_skip;
+    if (k.feat && stored) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat, k.feat_nt != 0);
     mlp_fwd_tile_src<true>(FragRing{P, fring[wave]}, feat, [&](int ob) { return c0sh_lds_load(c0l, ob, lane); },
-                           a, c2, lane, k.skip_dead && k.noise_f == nullptr);
-    if (k.feat) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m, k.feat_nt != 0);
+                           a, c2, lane, dead_skip, [&]() {
+                             if (k.feat && !stored) store_feat(k.feat, ray, kSc / 32 + tau, lane, feat, k.feat_nt != 0);
+                             stored = true;
+                           });
+    if (k.feat && stored) store_masks(k.feat, ray, kSc / 32 + tau, lane, a.m, k.feat_nt != 0);
     if (h == 0) {
       const float4 o4 = make_float4(c2[0], c2[1], c2[2], a.s1[0]);
       *reinterpret_cast<float4*>(rawb + 4 * q) = o4;

@@ -218,7 +218,7 @@ class RenderState:
     outputs, coarse origin of each fine sample, hash features, the workspace
     holding the packed weights)."""
     __slots__ = ("cfg", "rays", "noise_c", "noise_f", "table", "ws", "z_c", "z_f", "raw_c", "raw_f",
-                 "fine_src", "feat", "wsb", "nbytes", "bwd_args")
+                 "fine_src", "feat", "wsb", "nbytes", "bwd_args", "skip_dead")
 
 
 def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_feat, wsb=None,
@@ -230,7 +230,9 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
     repack=True since the last change of ws).  skip_dead_color (ABI 14, the
     trainer): tiles whose 32 raw sigmas are all <= 0 skip the colour net --
     rgb, depth, acc, the entropies and every gradient unchanged, the raw rgb
-    of those samples written as 0."""
+    of those samples written as 0 -- and such fine tiles' features are not
+    stored: the backward must then run with cfg.dense_bwd = 0 (render_bwd
+    refuses dense_bwd = 1 on such a state)."""
     L.require_device(rays, t_vals, t_rand, u, noise_c, noise_f, table, *ws)
     rays, t_vals, t_rand, u, noise_c, noise_f = (L.contig(t) for t in (rays, t_vals, t_rand, u,
                                                                       noise_c, noise_f))
@@ -278,6 +280,7 @@ def render_fwd(cfg, rays, t_vals, t_rand, u, noise_c, noise_f, table, ws, keep_f
         st.z_c, st.z_f, st.raw_c, st.raw_f = out["z_coarse"], out["z_fine"], out["raw_c"], out["raw_f"]
         st.fine_src, st.feat, st.wsb, st.nbytes = fine_src, feat, wsb, nbytes
         st.bwd_args = None
+        st.skip_dead = bool(skip_dead_color)
     return out, st
 
 
@@ -315,6 +318,9 @@ def render_bwd(st: RenderState, grads: dict, d_table, dws, overwrite: bool = Fal
     workspace, for a next render_fwd(wsb=st.wsb, weights_packed=True)."""
     B = st.rays.shape[0]
     dev = st.rays.device
+    if getattr(st, "skip_dead", False) and st.cfg.dense_bwd:
+        raise ValueError("hashnerf_amd.render_bwd: the forward ran with skip_dead_color (features of tiles "
+                         "without density not stored); the backward needs cfg.dense_bwd = 0")
     a = L.HnRenderBwdArgs()
     a.n_rays = B
     a.coarse = L.make_mlp(st.ws[:5])

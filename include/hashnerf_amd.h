@@ -210,8 +210,11 @@ typedef struct hn_render_fwd_args {
                                whose raw sigmas are all <= 0 -- alpha 0 and weight 0 at every sample,
                                so its colours enter no output and no gradient -- skips the colour
                                net: raw_c / raw_f rgb of those samples are written as 0 (rgb, depth,
-                               acc, the entropies and every gradient unchanged).  0 = every sample's
-                               raw rgb computed (the reference's `raw` output) */
+                               acc, the entropies and every gradient unchanged), and such fine
+                               tiles' features and ReLU masks are not stored in `feat` (no d raw of
+                               theirs is nonzero, so a dense_bwd = 0 backward never reads them; a
+                               dense_bwd = 1 backward of this state is invalid).  0 = every sample's
+                               raw rgb computed (the reference's `raw` output), every tile stored */
 } hn_render_fwd_args;
 
 typedef struct hn_render_bwd_args {

@@ -442,7 +442,9 @@ def test_zero_gradient_skip_bitwise(hn):
     HF.DEBUG_KEEP = True
     try:
         for dense in (1, 0, 0):
+            # the dense form's forward stores every tile's features (skip_dead_color off)
             tr._cfg.dense_bwd = dense
+            tr.dense_bwd = bool(dense)
             tr._fused_forward_backward(2000, batch)
             torch.cuda.synchronize()
             HF.L.check_device_faults()
