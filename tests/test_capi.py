@@ -215,3 +215,19 @@ def test_grid_sizes_bitexact_with_reference_formula(hn, oracle):
         for l in range(16):
             for a in range(3):
                 assert C.c_float(gs[l, a].item()).value == g.grid_size[l][a]
+
+
+def test_render_bwd_refuses_dense_after_skipping_forward(hn):
+    """A forward with skip_dead_color (the trainer's) stores no features for
+    fine tiles without density; functional.render_bwd refuses a dense_bwd = 1
+    backward of such a state before any launch (ABI 14 hn_render_fwd_args)."""
+    HF = hn.functional
+    box = (torch.tensor([-1.5, -1.5, -1.5]), torch.tensor([1.5, 1.5, 1.5]))
+    emb = hn.HashEmbedder(box, log2_hashmap_size=14, finest_resolution=64)
+    st = HF.RenderState()
+    st.cfg = HF.make_render_cfg(emb.grid(), True, False, True, scatter="binned")
+    st.rays = torch.zeros((4, 11))
+    st.skip_dead = True
+    st.cfg.dense_bwd = 1
+    with pytest.raises(ValueError, match="dense_bwd"):
+        HF.render_bwd(st, {}, None, [])
