@@ -105,11 +105,11 @@ struct B1K {
   float* lout;
   int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
   uint8_t* uflags;      // [B][kMarkB] marks (composite pre-pass): [0] coarse, [1] fine MLP tiles with a
-                        // nonzero d raw, [2] fine tiles with a nonzero sample or coarse twin (the
-                        // scatter's)
+                        // nonzero d raw, bits 16-27: the fine 16-sample groups with a nonzero
+                        // sample or coarse twin (the scatter's)
   int32_t* lmeta;       // work lists (render_lists_kernel): [0] coarse tiles, [1] fine tiles, [2] scatter
                         // tiles, [3] gsplit: the MLP waves g < gsplit run coarse tiles (slab_reduce_block)
-  int32_t* lists;       // coarse tile codes [2B] | fine tile codes [6B] | the scatter's tile codes [6B]
+  int32_t* lists;       // coarse tile codes [2B] | fine tile codes [6B] | the scatter's group codes [12B]
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -1649,8 +1649,8 @@ struct ScK {
   const float* draw;      // [B][64 + 192][4] d raw (composite pre-pass): zero = no feature grads to read
   int32_t scramble;       // the MLP backward's ray permutation (B1K::scramble; 0: identity)
   int32_t skip_zero;      // exact-zero skipping (!hn_render_cfg.dense_bwd)
-  const int32_t* lmeta;   // render_lists_kernel's counts ([2] scatter units, [3] the MLP waves' split)
-  const int32_t* slist;   // its scatter tile codes (ray << 3 | tile), or null: every unit
+  const int32_t* lmeta;   // render_lists_kernel's counts ([2] scatter groups, [3] the MLP waves' split)
+  const int32_t* slist;   // its scatter group codes (ray << 4 | 16-sample group), or null: every unit
   float* bins;
   int32_t bin_cap, bin_shift, nbins;
   // TV term (loss.py:11-43) as records of the same bins: tv_off[l] = first
@@ -1759,28 +1759,22 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
   bw.cap = (uint32_t)k.bin_cap;
   bw.shift = (uint32_t)k.bin_shift;
   // The block's units.  With exact-zero skipping: its slice of the list of
-  // fine tiles that have feature grads to scatter (render_lists_kernel, from
-  // the composite pre-pass's marks), the list in ray order and cut into equal
-  // slices over the blocks -- every block the same share of the work,
-  // whatever the scene leaves nonzero; a wave's unit is two consecutive tiles
-  // of the slice, lanes 0-31 the first, 32-63 the second (often of different
-  // rays; the 16-lane run rows never cross them), and each wave holds its
-  // units' codes in registers (lane j: round j).  Otherwise (dense_bwd) every
-  // unit is a third of one ray's fine samples, the rays permuted as the MLP
-  // backward's (unit_ray).
+  // fine 16-sample groups that have feature grads to scatter
+  // (render_lists_kernel, from the composite pre-pass's marks), the list in
+  // ray order and cut into equal slices over the blocks -- every block the
+  // same share of the work, whatever the scene leaves nonzero; a wave's unit
+  // is four consecutive groups of the slice, one per 16-lane run row (often of
+  // different rays; runs never cross rows, so the records are the dense
+  // form's).  Otherwise (dense_bwd) every unit is a third of one ray's fine
+  // samples, the rays permuted as the MLP backward's (unit_ray).
   const bool use_list = k.slist != nullptr;
   int64_t u0 = 0, u1 = 0;
-  // lane j: the codes of this wave's two tiles of round j (-1: none)
-  int ucode0 = -1, ucode1 = -1;
+  int64_t s0 = 0, s1 = 0;   // this block's slice of the group list
   if (use_list) {
     const int64_t Ns = __builtin_amdgcn_readfirstlane(k.lmeta[2]);
-    const int64_t s0 = (int64_t)blockIdx.x * Ns / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * Ns / gridDim.x;
-    u1 = (s1 - s0 + 1) / 2;   // a unit = two consecutive tiles of the slice, one per lane half
-    const int64_t uj = wave + (int64_t)lane * kScWaves;
-    if (uj < u1) {
-      ucode0 = k.slist[s0 + 2 * uj];
-      if (s0 + 2 * uj + 1 < s1) ucode1 = k.slist[s0 + 2 * uj + 1];
-    }
+    s0 = (int64_t)blockIdx.x * Ns / gridDim.x;
+    s1 = (int64_t)(blockIdx.x + 1) * Ns / gridDim.x;
+    u1 = (s1 - s0 + 3) / 4;   // a unit = four consecutive groups of the slice, one per 16-lane row
   } else {
     const int64_t units = 3 * k.B;
     const int64_t per = (units + gridDim.x - 1) / gridDim.x;
@@ -1869,11 +1863,15 @@ __global__ __launch_bounds__(64 * kScWaves) void scatter_bins_kernel(ScK k) {
       int i;   // the lane's fine sample
       bool none = false;   // a second tile that does not exist: no grads
       if (use_list) {
-        const int ca = __builtin_amdgcn_readlane(ucode0, (int)it), cb = __builtin_amdgcn_readlane(ucode1, (int)it);
-        none = lane >= 32 && cb < 0;
-        const int code = lane < 32 || cb < 0 ? ca : cb;
-        ray = code >> 3;
-        i = 32 * (code & 7) + (lane & 31);
+        // row r of the unit: group s0 + 4 u + r, a group of 16 consecutive
+        // samples of one ray -- the run rows are the dense form's, so the
+        // records are too (minus the all-zero ones)
+        const int64_t gj = s0 + 4 * u + (lane >> 4);
+        const int c0 = k.slist[s0 + 4 * u];
+        const int code = gj < s1 ? k.slist[gj] : c0;
+        none = gj >= s1;
+        ray = code >> 4;
+        i = 16 * (code & 15) + (lane & 15);
       } else {
         ray = unit_ray(u / 3);
         i = 64 * (int)(u % 3) + lane;
@@ -2490,16 +2488,19 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
     // (the same point, fine_src < 64), has a nonzero d raw -- the tile has
     // feature grads to scatter (scatter_bins_kernel's lists)
     const unsigned long long cm = cmask[wave >> 1];
-    uint32_t su = 0u;   // bit t: fine tile t (32 samples) has feature grads to scatter
+    uint32_t su = 0u;   // bit t: fine 16-sample group t has feature grads to scatter
     for (int j = lane; j < kSf; j += 64) {
       const int src = k.fine_src[ray * kSf + j];
       const bool nz = draw_nonzero(*reinterpret_cast<const float4*>(rawb + 4 * j)) ||
                       (src < kSc && ((cm >> src) & 1ull) != 0ull);
       const uint64_t b = __ballot(nz);
-      su |= ((uint32_t)b != 0u ? 1u : 0u) << (2 * (j >> 6));
-      su |= ((uint32_t)(b >> 32) != 0u ? 1u : 0u) << (2 * (j >> 6) + 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) su |= (((b >> (16 * q)) & 0xffffull) != 0ull ? 1u : 0u) << (4 * (j >> 6) + q);
     }
-    if (lane == 0) k.uflags[kMarkB * ray + 2] = (uint8_t)su;
+    if (lane == 0) {
+      k.uflags[kMarkB * ray + 2] = (uint8_t)su;
+      k.uflags[kMarkB * ray + 3] = (uint8_t)(su >> 8);
+    }
   }
 }
 
@@ -2637,9 +2638,9 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   static_assert(kListThreads == 256, "list_block_scan: 4 waves");
   __shared__ int sh[3][4];
   const int t = threadIdx.x;
-  // bytes [coarse tiles (2 bits), fine tiles (6), the scatter's fine tiles (6), -]
+  // bits [coarse tiles (2), -, fine tiles (6), -, the scatter's 16-sample groups (12), -]
   auto mword = [&](int64_t r) -> uint32_t {
-    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0x3f3f03u;
+    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0xfff3f03u;
   };
   const int64_t R = (k.B + gridDim.x - 1) / gridDim.x;
   const int64_t ra = (int64_t)blockIdx.x * R, rb = ra + R < k.B ? ra + R : k.B;
@@ -2648,7 +2649,7 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   for (int64_t r = t; r < k.B; r += kListThreads) {
     const uint32_t w = mword(r);
     const int c = __builtin_popcount(w & 3u), f = __builtin_popcount((w >> 8) & 63u),
-              g = __builtin_popcount((w >> 16) & 63u);
+              g = __builtin_popcount((w >> 16) & 0xfffu);
     tc += c; tf += f; ts += g;
     if (r < ra) { bc += c; bf += f; bs += g; }
   }
@@ -2661,15 +2662,15 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
     const int64_t r = r0 + t;
     const uint32_t w = r < rb ? mword(r) : 0u;
     const int c = __builtin_popcount(w & 3u), f = __builtin_popcount((w >> 8) & 63u),
-              g = __builtin_popcount((w >> 16) & 63u);
+              g = __builtin_popcount((w >> 16) & 0xfffu);
     const int ic = list_block_scan(c, sh[0]), jf = list_block_scan(f, sh[1]), ks = list_block_scan(g, sh[2]);
     int64_t oc = xc + ic - c, of = xf + jf - f, os = xs + ks - g;
     for (int i = 0; i < 2; ++i)
       if ((w >> i) & 1u) lc[oc++] = (int32_t)(r << 3) | i;
     for (int i = 0; i < 6; ++i)
       if ((w >> (8 + i)) & 1u) lf[of++] = (int32_t)(r << 3) | i;
-    for (int i = 0; i < 6; ++i)
-      if ((w >> (16 + i)) & 1u) ls[os++] = (int32_t)(r << 3) | i;
+    for (int i = 0; i < 12; ++i)
+      if ((w >> (16 + i)) & 1u) ls[os++] = (int32_t)(r << 4) | i;
     xc += list_block_sum(c, sh[0]);
     xf += list_block_sum(f, sh[1]);
     xs += list_block_sum(g, sh[2]);
@@ -3292,7 +3293,8 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4 +
-              ((15 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists [14n]
+              ((21 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists
+                                                 // [(2 + 6 + 12) n]
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -3649,9 +3651,8 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.scramble = k.scramble;
     sk.skip_zero = k.skip_zero;
     sk.lmeta = k.lmeta;
-    // the scatter's unit list (each wave holds <= 64 rounds of codes in a register)
-    sk.slist = k.skip_zero && (6 * a->n_rays + kBwdBlocks - 1) / kBwdBlocks <= 2 * 64 * kScWaves
-                   ? k.lists + 8 * a->n_rays : nullptr;
+    // the scatter's group list
+    sk.slist = k.skip_zero ? k.lists + 8 * a->n_rays : nullptr;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
     sk.dfeat_f = k.dfeat_f;
