@@ -105,11 +105,12 @@ struct B1K {
   float* lout;
   int32_t skip_zero;    // exact-zero skipping (!hn_render_cfg.dense_bwd)
   uint8_t* uflags;      // [B][kMarkB] marks (composite pre-pass): [0] coarse, [1] fine MLP tiles with a
-                        // nonzero d raw, bits 16-27: the fine 16-sample groups with a nonzero
-                        // sample or coarse twin (the scatter's)
+                        // nonzero d raw -- as bits: 0-3 coarse 16-sample groups, 8-19 fine
+                        // groups (the MLP backward's), 20-31 fine groups with a nonzero sample or
+                        // coarse twin (the scatter's)
   int32_t* lmeta;       // work lists (render_lists_kernel): [0] coarse tiles, [1] fine tiles, [2] scatter
                         // tiles, [3] gsplit: the MLP waves g < gsplit run coarse tiles (slab_reduce_block)
-  int32_t* lists;       // coarse tile codes [2B] | fine tile codes [6B] | the scatter's group codes [12B]
+  int32_t* lists;       // group codes (ray << 4 | group): coarse [4B] | fine [12B] | the scatter's [12B]
 };
 
 // Backward schedules (render_bwd_kernel MODE):
@@ -959,7 +960,7 @@ HN_DEV void tile_lds_order() {
 // images (read back as the c0 accumulators' seed, 8 broadcast ds_read_b128
 // per tile) instead of 32 VGPRs live across the unit's tiles.
 constexpr int kC0shF = kNImg * kImgBlk / 4;   // float offset in the wave's slab
-static_assert(kC0shF + 64 <= kRRows * kXS, "c0sh fits the per-wave slab");
+static_assert(kC0shF + 128 <= kRRows * kXS, "c0sh (two groups' rays) fits the per-wave slab");
 struct C0Sh {
   const float* lds;
 };
@@ -2339,21 +2340,31 @@ HN_DEV void b1_unit(const B1K& k, int64_t ray, int part, float* X, DW& dw, WRing
 // new_ray: the previous tile of this wave was another ray's (or none), so
 // the ray's SH operand image and color_net.0's SH rows (c0sh) are set up;
 // otherwise they are still in the wave's LDS from that tile.
-HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int tile, bool fine, float* X, DW& dw, WRing& wr,
-                          bool new_ray = true) {
+// One MLP tile of two listed 16-sample groups (round 6): points 0-15 group
+// code ca, 16-31 group cb (codes ray << 4 | group; cb < 0: none, those lanes
+// run with d raw 0 and store nothing).  Each lane's ray gives its own SH
+// columns, and color_net.0's SH half is formed for both groups' rays at once
+// (column p of that product is point p's ray), kept in LDS per group.  The
+// two groups are often of different rays; every per-point input (features,
+// masks, d raw) is read at the point's own place in the ray's tiles and its
+// feature grads are written there, so the dW products and grads are those of
+// the dense form's tiles, grouped differently.
+HN_DEV void b1_groups(const B1K& k, int ca, int cb, bool fine, float* X, DW& dw, WRing& wr) {
   const int lane = lane_id();
   const int p = lane & 31, h = lane >> 5;
-  const float4 dr = *reinterpret_cast<const float4*>(
-      k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + 32 * tile + p) * 4);
+  const bool none = p >= 16 && cb < 0;
+  const int code = p < 16 || cb < 0 ? ca : cb;
+  const int64_t ray = code >> 4;
+  const int i = 16 * (code & 15) + (p & 15);          // the point within its pass
+  float4 dr = *reinterpret_cast<const float4*>(k.draw + ((size_t)ray * (kSc + kSf) + (fine ? kSc : 0) + i) * 4);
+  if (none) dr = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* P = opaque_ptr(fine ? k.Pf : k.Pc);
   C0Sh c0sh;
-  c0sh.lds = X + kC0shF;
-  if (new_ray) {
-  Ray r;
-  load_ray(k.rays, ray, r);
-  float sh8[8], shx8[8];
-  ray_sh(r, h, sh8, shx8);
   {
+    Ray r;
+    load_ray(k.rays, ray, r);
+    float sh8[8], shx8[8];
+    ray_sh(r, h, sh8, shx8);
     const SP<2> sp = splitn<2>([&](int j) { return shx8[j]; });
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -2361,34 +2372,47 @@ HN_DEV void b1_unit_split(const B1K& k, int64_t ray, int tile, bool fine, float*
       put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h, w[0], w[1]);
       put_quad(reinterpret_cast<char*>(X), kBC0in, q, p, 2 * h + 1, w[2], w[3]);
     }
-  }
-  {
     float* cl = X + kC0shF;
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
       const f32x16 v = gemm<R_F2S>(P, ob, zero16(), lane, [&](int s) { return sh8[s]; });
-      if (p == 0)
+      if ((p & 15) == 0)   // columns 0 and 16: the two groups' rays
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<f32x4*>(cl + 32 * ob + row_of(4 * g, h)) =
+          *reinterpret_cast<f32x4*>(cl + 64 * (p >> 4) + 32 * ob + row_of(4 * g, h)) =
               f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
     }
     lds_fence_wave();
+    c0sh.lds = cl + 64 * (p >> 4);
   }
-  }
-  const int ctile = (fine ? kSc / 32 : 0) + tile;
+  // the point's place in the saved tiles: tile (pass offset + i / 32), lane (i % 32) + 32 h
+  const int ctile = (fine ? kSc / 32 : 0) + (i >> 5), pl = (i & 31) + 32 * h;
+  const float* fb = k.feat + (size_t)ray * HN_RENDER_FEAT_PER_RAY;
   f32x16 feat;
-  load_feat(k.feat, ray, ctile, lane, feat);
-  uint32_t sm[3] = {0u, 0u, 0u};
-  load_masks(k.feat, ray, ctile, lane, sm);
-  const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, dr, dw, sm);
-  // this tile's feature grads (the saved-feature tile order of both passes)
-  f32x4* dst = fine ? reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + tile) * 1024)
-                    : reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)tile * 1024);
+  {
+    const f32x4* t = reinterpret_cast<const f32x4*>(fb + (size_t)ctile * 1024);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const f32x4 v = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
-    __builtin_nontemporal_store(v, dst + 64 * c + lane);   // read once, by the scatter
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 v = __builtin_nontemporal_load(t + 64 * c + pl);
+      feat[4 * c] = v.x; feat[4 * c + 1] = v.y; feat[4 * c + 2] = v.z; feat[4 * c + 3] = v.w;
+    }
+  }
+  uint32_t sm[3];
+  {
+    const uint32_t* t = reinterpret_cast<const uint32_t*>(fb + kTilesPerRay * 1024) + ctile * kMaskWordsPerTile;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sm[j] = __builtin_nontemporal_load(t + 64 * j + pl);
+  }
+  const f32x16 dfeat = b1_tile(P, wr, X, feat, c0sh, dr, dw, sm);
+  // this point's feature grads (the saved-feature tile order of both passes)
+  if (!none) {
+    f32x4* dst = fine ? reinterpret_cast<f32x4*>(k.dfeat_f + ((size_t)ray * (kSf / 32) + (i >> 5)) * 1024)
+                      : reinterpret_cast<f32x4*>(k.dfeat + (size_t)ray * kDcRay + (size_t)(i >> 5) * 1024);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 v = f32x4{dfeat[4 * c], dfeat[4 * c + 1], dfeat[4 * c + 2], dfeat[4 * c + 3]};
+      __builtin_nontemporal_store(v, dst + 64 * c + pl);   // read once, by the scatter
+    }
   }
 }
 
@@ -2423,6 +2447,7 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
   // coarse wave's nonzero-sample mask reaches the fine wave through LDS
   __shared__ unsigned long long cmask[kFwdWaves / 2];
   const bool active = w < 2 * k.B;
+  uint32_t nzf = 0u;   // the fine wave's MLP groups
   const int64_t ray = w >> 1;
   const bool fine = (w & 1) != 0;
   float* rawb = lds[wave] + kSf;
@@ -2471,15 +2496,16 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
     else
       composite_bwd<kSc / 64>(rawb, zb, noise, S, r.dnorm, k.white != 0, g, nullptr, graw, rawb, lane);
     lds_fence_wave();
-    uint32_t nzu = 0u;   // bit t: a sample of MLP tile t (32 samples) has a nonzero d raw
+    uint32_t nzu = 0u;   // bit t: a sample of 16-sample group t has a nonzero d raw (the MLP's)
     for (int j = lane; j < S; j += 64) {
       const float4 d = *reinterpret_cast<const float4*>(rawb + 4 * j);
       *reinterpret_cast<float4*>(dst + 4 * j) = d;
       const uint64_t b = __ballot(draw_nonzero(d));
-      nzu |= ((uint32_t)b != 0u ? 1u : 0u) << (2 * (j >> 6));
-      nzu |= ((uint32_t)(b >> 32) != 0u ? 1u : 0u) << (2 * (j >> 6) + 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nzu |= (((b >> (16 * q)) & 0xffffull) != 0ull ? 1u : 0u) << (4 * (j >> 6) + q);
     }
-    if (lane == 0) k.uflags[kMarkB * ray + (fine ? 1 : 0)] = (uint8_t)nzu;
+    if (lane == 0 && !fine) k.uflags[kMarkB * ray] = (uint8_t)nzu;   // byte 0: the coarse groups
+    nzf = nzu;
     if (!fine) cmask[wave >> 1] = __ballot(draw_nonzero(*reinterpret_cast<const float4*>(rawb + 4 * lane)));
   }
   __syncthreads();
@@ -2497,9 +2523,11 @@ __global__ __launch_bounds__(256) void render_comp_bwd_kernel(B1K k) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) su |= (((b >> (16 * q)) & 0xffffull) != 0ull ? 1u : 0u) << (4 * (j >> 6) + q);
     }
-    if (lane == 0) {
-      k.uflags[kMarkB * ray + 2] = (uint8_t)su;
-      k.uflags[kMarkB * ray + 3] = (uint8_t)(su >> 8);
+    if (lane == 0) {   // bits 8-19: the fine MLP groups, 20-31: the scatter's groups
+      const uint32_t v = nzf | (su << 12);
+      k.uflags[kMarkB * ray + 1] = (uint8_t)v;
+      k.uflags[kMarkB * ray + 2] = (uint8_t)(v >> 8);
+      k.uflags[kMarkB * ray + 3] = (uint8_t)(v >> 16);
     }
   }
 }
@@ -2601,9 +2629,10 @@ HN_DEV void dw_add_lds(DW& dw, const f32x4* L, int lane) {
 }
 
 // The backward's work lists (round 6), from the composite pre-pass's marks
-// (B1K::uflags; every tile with dense_bwd): the coarse tiles, the fine tiles
-// and the scatter's fine tiles with feature grads, each in ray order, as
-// codes (ray << 3 | tile); their lengths and the MLP waves' coarse / fine
+// (B1K::uflags; every group with dense_bwd): the coarse and the fine 16-sample
+// groups with a nonzero d raw (the MLP backward's) and the fine groups with
+// feature grads (the scatter's), each in ray order, as
+// codes (ray << 4 | 16-sample group); their lengths and the MLP waves' coarse / fine
 // split.  Workgroup w writes the codes of rays [w R, (w + 1) R): it counts
 // the marks of every earlier ray itself (a few loads per thread; no
 // workgroup waits for another), then takes 256 rays at a time, one per
@@ -2638,9 +2667,9 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   static_assert(kListThreads == 256, "list_block_scan: 4 waves");
   __shared__ int sh[3][4];
   const int t = threadIdx.x;
-  // bits [coarse tiles (2), -, fine tiles (6), -, the scatter's 16-sample groups (12), -]
+  // bits [coarse groups (4), -, fine groups (12), the scatter's groups (12)]
   auto mword = [&](int64_t r) -> uint32_t {
-    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0xfff3f03u;
+    return k.skip_zero ? *reinterpret_cast<const uint32_t*>(k.uflags + kMarkB * r) : 0xffffff0fu;
   };
   const int64_t R = (k.B + gridDim.x - 1) / gridDim.x;
   const int64_t ra = (int64_t)blockIdx.x * R, rb = ra + R < k.B ? ra + R : k.B;
@@ -2648,29 +2677,29 @@ __global__ __launch_bounds__(kListThreads) void render_lists_kernel(B1K k) {
   int bc = 0, bf = 0, bs = 0, tc = 0, tf = 0, ts = 0;
   for (int64_t r = t; r < k.B; r += kListThreads) {
     const uint32_t w = mword(r);
-    const int c = __builtin_popcount(w & 3u), f = __builtin_popcount((w >> 8) & 63u),
-              g = __builtin_popcount((w >> 16) & 0xfffu);
+    const int c = __builtin_popcount(w & 15u), f = __builtin_popcount((w >> 8) & 0xfffu),
+              g = __builtin_popcount(w >> 20);
     tc += c; tf += f; ts += g;
     if (r < ra) { bc += c; bf += f; bs += g; }
   }
   int64_t xc = list_block_sum(bc, sh[0]), xf = list_block_sum(bf, sh[1]), xs = list_block_sum(bs, sh[2]);
   const int64_t Nc = list_block_sum(tc, sh[0]), Nf = list_block_sum(tf, sh[1]), Ns = list_block_sum(ts, sh[2]);
   int32_t* lc = k.lists;
-  int32_t* lf = lc + 2 * k.B;
-  int32_t* ls = lf + 6 * k.B;
+  int32_t* lf = lc + 4 * k.B;
+  int32_t* ls = lf + 12 * k.B;
   for (int64_t r0 = ra; r0 < rb; r0 += kListThreads) {
     const int64_t r = r0 + t;
     const uint32_t w = r < rb ? mword(r) : 0u;
-    const int c = __builtin_popcount(w & 3u), f = __builtin_popcount((w >> 8) & 63u),
-              g = __builtin_popcount((w >> 16) & 0xfffu);
+    const int c = __builtin_popcount(w & 15u), f = __builtin_popcount((w >> 8) & 0xfffu),
+              g = __builtin_popcount(w >> 20);
     const int ic = list_block_scan(c, sh[0]), jf = list_block_scan(f, sh[1]), ks = list_block_scan(g, sh[2]);
     int64_t oc = xc + ic - c, of = xf + jf - f, os = xs + ks - g;
-    for (int i = 0; i < 2; ++i)
-      if ((w >> i) & 1u) lc[oc++] = (int32_t)(r << 3) | i;
-    for (int i = 0; i < 6; ++i)
-      if ((w >> (8 + i)) & 1u) lf[of++] = (int32_t)(r << 3) | i;
+    for (int i = 0; i < 4; ++i)
+      if ((w >> i) & 1u) lc[oc++] = (int32_t)(r << 4) | i;
     for (int i = 0; i < 12; ++i)
-      if ((w >> (16 + i)) & 1u) ls[os++] = (int32_t)(r << 4) | i;
+      if ((w >> (8 + i)) & 1u) lf[of++] = (int32_t)(r << 4) | i;
+    for (int i = 0; i < 12; ++i)
+      if ((w >> (20 + i)) & 1u) ls[os++] = (int32_t)(r << 4) | i;
     xc += list_block_sum(c, sh[0]);
     xf += list_block_sum(f, sh[1]);
     xs += list_block_sum(g, sh[2]);
@@ -2764,20 +2793,22 @@ void render_bwd_kernel(B1K k) {
     const bool fine = g_me >= gc;                            // wave-uniform
     const int64_t N = fine ? Nf : Nc;
     const int gi = fine ? g_me - gc : g_me, GG = fine ? G - gc : gc;
-    const int64_t lo = GG ? (int64_t)gi * N / GG : 0, hi = GG ? (int64_t)(gi + 1) * N / GG : 0;
-    const int32_t* L = k.lists + (fine ? 2 * k.B : 0);
+    // slices of whole group pairs (a tile = two consecutive listed groups)
+    const int64_t NP = (N + 1) / 2;
+    const int64_t lo = GG ? 2 * ((int64_t)gi * NP / GG) : 0, hi2 = GG ? 2 * ((int64_t)(gi + 1) * NP / GG) : 0;
+    const int64_t hi = hi2 < N ? hi2 : N;
+    const int32_t* L = k.lists + (fine ? 4 * k.B : 0);
     wring_prime(wr, fine ? k.Pf : k.Pc, lane);
 #ifndef HN_DIAG_NOTILES
 #define HN_DIAG_NOTILES 0   // diagnostic builds: 1 = no tiles
 #endif
-    int prev = -1;   // the ray of this wave's previous tile (its SH set-up is reused)
-    for (int64_t c0 = lo; c0 < (HN_DIAG_NOTILES ? lo : hi); c0 += 64) {
+    for (int64_t c0 = lo; c0 < (HN_DIAG_NOTILES ? lo : hi); c0 += 64) {   // lo even: pairs never straddle
       const int cnt = (int)(hi - c0 < 64 ? hi - c0 : 64);
-      const int codes = lane < cnt ? L[c0 + lane] : 0;
-      for (int j = 0; j < cnt; ++j) {
-        const int code = __builtin_amdgcn_readlane(codes, j);
-        b1_unit_split(k, (int64_t)(code >> 3), code & 7, fine, X, dw, wr, (code >> 3) != prev);
-        prev = code >> 3;
+      const int codes = lane < cnt ? L[c0 + lane] : -1;
+      for (int j = 0; j < cnt; j += 2) {
+        const int ca = __builtin_amdgcn_readlane(codes, j);
+        const int cb = j + 1 < cnt ? __builtin_amdgcn_readlane(codes, j + 1) : -1;
+        b1_groups(k, ca, cb, fine, X, dw, wr);
       }
     }
     if (HN_DW_BLOCKRED) {
@@ -3293,8 +3324,8 @@ static WsLayout ws_layout(const hn_render_cfg* cfg, int64_t n_rays, int mode) {
   const size_t n = n_rays > 0 ? (size_t)n_rays : 0;
   WsLayout w;
   w.dfeat_f = (size_t)2 * G_END + (size_t)kBwdBlocks * kSlabSlots * W_END + n * kDcRay + n * (kSc + kSf) * 4 +
-              ((21 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists
-                                                 // [(2 + 6 + 12) n]
+              ((29 * n + 8 + 3) & ~(size_t)3);   // + the marks [n][4] u8, the lists' counts [8], the lists
+                                                 // [(4 + 12 + 12) n]
   w.bins = w.dfeat_f + (mode == kModeSplit ? n * kSf * 32 : 0);
   w.total = w.bins + (mode == kModeSplit ? bin_geom(cfg->grid.log2_hashmap_size, n_rays, cfg->bin_cap).floats : 0);
   return w;
@@ -3652,7 +3683,7 @@ extern "C" int32_t hn_render_bwd(const hn_render_cfg* cfg, const hn_render_bwd_a
     sk.skip_zero = k.skip_zero;
     sk.lmeta = k.lmeta;
     // the scatter's group list
-    sk.slist = k.skip_zero ? k.lists + 8 * a->n_rays : nullptr;
+    sk.slist = k.skip_zero ? k.lists + 16 * a->n_rays : nullptr;
     sk.z_fine = a->z_fine;
     sk.fine_src = a->fine_src;
     sk.dfeat_f = k.dfeat_f;
