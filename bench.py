@@ -78,8 +78,9 @@ N_SIMDS = 1024                   # 256 CUs x 4 SIMDs
 # the kernels of one hn_render_bwd launch, per table-gradient scatter
 BWD_KERNELS = {"atomic": ("render_comp_bwd_kernel", "render_bwd_kernel", "slab_reduce_kernel"),
                # binned: the dW slab reduction runs inside scatter_bins_kernel (HN_SC_SLAB)
-               "binned": ("render_comp_bwd_kernel", "render_bwd_kernel", "scatter_bins_kernel",
-                          "ovf_place_kernel", "bin_reduce_kernel")}
+               # render_lists_kernel (round 6): the exact-zero skipping's work lists
+               "binned": ("render_comp_bwd_kernel", "render_lists_kernel", "render_bwd_kernel",
+                          "scatter_bins_kernel", "ovf_place_kernel", "bin_reduce_kernel")}
 
 
 def measured_traffic(cfg_id, n_rand_override, scene, pretrain, scatter):
@@ -93,7 +94,9 @@ def measured_traffic(cfg_id, n_rand_override, scene, pretrain, scatter):
         return None, None, None, {}
     t = json.load(open(path))
     ks = t.get("kernels", {})
-    kern = [k for k in BWD_KERNELS[scatter] if k != "ovf_place_kernel" or k in ks]   # returns at once w/o spills
+    # ovf_place_kernel returns at once without spills; render_lists_kernel runs only
+    # with exact-zero skipping (and files of older libraries lack it)
+    kern = [k for k in BWD_KERNELS[scatter] if k not in ("ovf_place_kernel", "render_lists_kernel") or k in ks]
     if not all(k in ks and "fetch_bytes" in ks[k] for k in kern):
         return None, None, None, ks
     return (sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in kern), t.get("source"),
